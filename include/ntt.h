@@ -1,0 +1,105 @@
+/* C ABI of libntt.so — the MI355X-native drop-in for the reference's NTT host entry points.
+ *
+ * The reference (tie-pilot-qxw/NTT) has no library API: its entry points are C++ host drivers called
+ * from main().  Each function below names the reference interface it replaces.
+ *
+ *   SSIP(long long* x, long long omega, uint log_n)            GZKP-NTT.cu:1452 (= self-sort-in-place.cu:309)
+ *   NTT_GZKP<TPI,BITS>(cgbn_mem_t<bits> data[], uint len, uint2 reverse[], uint reverse_len,
+ *                      cgbn_mem_t<bits> prime, cgbn_mem_t<bits> omega, uint B, uint G)
+ *                                                               big-num.cu:260-261
+ *   NTT_GZKP(long long data[], longlong2 reverse[], long long len, long long omega, int B, int G,
+ *            long long reverse_num)                             parallel-load.cu:195 / GZKP-NTT.cu:167
+ *   inverse: NTT(..., inv(root)) then * inv(len)               GZKP-NTT.cu:1725-1732 (commented out)
+ *
+ * Conventions (same as the reference unless stated):
+ *   - data is a DEVICE pointer owned by the caller; transforms are in place, natural order in and
+ *     out (the reference's SSIP contract), elements canonical (< p), not in Montgomery form;
+ *   - element layout = cgbn_mem_t<32*W>: W little-endian 32-bit words (cgbn_cuda.h:51-55), i.e.
+ *     limbs64 little-endian 64-bit limbs; the 1-limb P469762049 path uses `long long` elements;
+ *   - `omega` arguments are the multiplicative GENERATOR (the reference passes `root`, 3), the
+ *     n-th root is omega^((p-1)/n) (GZKP-NTT.cu:1462, big-num.cu:292-296);
+ *   - unlike the reference (void, prints timings, default stream, blocking): every call returns a
+ *     status (0 ok, < 0 error, see ntt_strerror), prints nothing, and the plan API is asynchronous
+ *     on the given hipStream_t (NULL = default stream).  The reference-shaped shims SSIP /
+ *     NTT_GZKP_256 keep the reference's blocking behaviour.
+ *   - plans are thread-compatible: one plan per thread, or serialise calls on a plan.
+ */
+#ifndef NTT_AMD_NTT_H
+#define NTT_AMD_NTT_H
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes */
+#define NTT_OK 0
+#define NTT_ERR_ARG (-1)      /* invalid field / size / limb count / pointer */
+#define NTT_ERR_HIP (-2)      /* HIP runtime error (launch, allocation, copy) */
+#define NTT_ERR_RCCL (-3)     /* RCCL error (multi-GPU) */
+#define NTT_ERR_FIELD (-4)    /* modulus unsupported (even, too large, no root of unity of order n) */
+#define NTT_ERR_NODEV (-5)    /* no HIP device */
+
+/* field ids */
+#define NTT_FIELD_P469762049 0   /* 7*2^26+1, generator 3 (GZKP-NTT.cu:7-8) */
+#define NTT_FIELD_BN254_FR 1     /* 0x30644e72...f0000001, generator 5 */
+#define NTT_FIELD_BLS12_381_FR 2 /* 0x73eda753...00000001, generator 7 */
+
+typedef struct ntt_plan ntt_plan;
+
+/* Create a plan for 2^log_n-point transforms on `device` (twiddle tables and scratch are cached in
+ * the plan: the reference rebuilt its tables on every call, GZKP-NTT.cu:1476-1500).
+ * limbs64: 1 (P469762049 only, `long long` elements), 4 (256-bit, cgbn_mem_t<256>), 6 (384-bit
+ * template).  Replaces the table setup inside SSIP (GZKP-NTT.cu:1452-1505) and NTT_GZKP
+ * (big-num.cu:278-309). */
+int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device);
+
+/* Modulus-generic plan, like big-num.cu's `prime` / `omega` kernel arguments (big-num.cu:68,173,260):
+ * modulus and generator given as limbs64 little-endian 64-bit limbs. */
+int ntt_plan_create_custom(ntt_plan** out, const uint64_t* modulus, const uint64_t* generator, unsigned limbs64,
+                           unsigned log_n, int device);
+
+/* Forward NTT in place, natural -> natural (SSIP GZKP-NTT.cu:1452, NTT_GZKP big-num.cu:260). */
+int ntt_forward(ntt_plan* plan, void* d_data, void* hip_stream);
+/* Inverse NTT in place including the n^-1 scale (GZKP-NTT.cu:1725-1732). */
+int ntt_inverse(ntt_plan* plan, void* d_data, void* hip_stream);
+/* `batch` independent transforms laid out back to back (stride 2^log_n elements). */
+int ntt_forward_batch(ntt_plan* plan, void* d_data, unsigned batch, void* hip_stream);
+int ntt_inverse_batch(ntt_plan* plan, void* d_data, unsigned batch, void* hip_stream);
+
+/* Pointwise product c = a * b mod p over 2^log_n elements (polynomial-multiply middle step). */
+int ntt_pointwise_mul(ntt_plan* plan, const void* d_a, const void* d_b, void* d_c, void* hip_stream);
+/* Cyclic polynomial product c = a * b of length 2^log_n: forward(a), forward(b), pointwise, inverse.
+ * a and b are overwritten with their transforms. */
+int ntt_polymul(ntt_plan* plan, void* d_a, void* d_b, void* d_c, void* hip_stream);
+
+/* Fill a device vector with the SURVEY §8d synthetic inputs: kind 0 = x_j = j (the reference's
+ * input, GZKP-NTT.cu:1587), kind 1 = SplitMix64 limbs with the top limb masked (seeded). */
+int ntt_fill(ntt_plan* plan, void* d_data, int kind, uint64_t seed, void* hip_stream);
+
+/* Plan introspection: n, bytes per element, number of passes and their log2 radices. */
+int ntt_plan_info(const ntt_plan* plan, uint64_t* n, unsigned* elem_bytes, unsigned* npasses, unsigned radix_log[8]);
+int ntt_plan_destroy(ntt_plan* plan);
+const char* ntt_strerror(int status);
+
+/* ---------------------------------------------------------------- reference-shaped shims */
+/* SSIP(x, omega, log_n): P469762049 path, long long elements in device memory, blocking,
+ * default stream (GZKP-NTT.cu:1452).  Prints nothing; errors are reported by the return value of
+ * ntt_last_error(). */
+void SSIP(long long* x, long long omega, unsigned log_n);
+/* NTT_GZKP<8,256>(data, len, reverse, reverse_len, prime, omega, B, G) (big-num.cu:260): 256-bit
+ * elements (8 x u32 LE), any odd prime < 2^255 given as 8 u32 words, omega = generator.  reverse /
+ * reverse_len / B / G are accepted for signature compatibility and ignored (the transform is
+ * self-sorting).  Blocking, default stream.  Returns a status. */
+int NTT_GZKP_256(uint32_t* data, uint32_t len, const void* reverse, uint32_t reverse_len, const uint32_t prime[8],
+                 const uint32_t omega[8], uint32_t B, uint32_t G);
+/* NTT_GZKP(data, reverse, len, omega, B, G, reverse_num) for P469762049 (parallel-load.cu:195). */
+int NTT_GZKP_64(long long* data, const void* reverse, long long len, long long omega, int B, int G,
+                long long reverse_num);
+int ntt_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,561 @@
+// Host side of libntt.so: plans (twiddle tables + scratch cached per device), pass scheduling, the
+// C ABI of include/ntt.h and the reference-shaped shims (SSIP, NTT_GZKP_256, NTT_GZKP_64).
+//
+// Reference behaviour mirrored (file:line in tie-pilot-qxw/NTT):
+//   * w_n = g^((p-1)/n) from the generator argument        GZKP-NTT.cu:1462, big-num.cu:292-296
+//   * forward = natural -> natural, in place               SSIP GZKP-NTT.cu:1452-1558
+//   * inverse = forward with g^-1, then * n^-1             GZKP-NTT.cu:1725-1732
+//   * modulus-generic 256-bit path (prime argument)        big-num.cu:68,173,260
+// Differences: tables are built once per plan (the reference rebuilt pq/omegas on every call and
+// freed them with a new[]/free mismatch, GZKP-NTT.cu:1554-1555); errors are returned as status
+// codes instead of asserts; nothing is printed.
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <tuple>
+#include <vector>
+
+#include "../../include/ntt.h"
+#include "ntt_kernels.hpp"
+
+using namespace ntt;
+
+namespace {
+
+thread_local int g_last_error = NTT_OK;
+
+// ------------------------------------------------------------------------------ host field math
+template <int N>
+using Vec = std::array<uint32_t, N>;
+
+template <int N>
+struct HostField {
+  Modulus<N> M;
+  Vec<N> r1{}, r2{};  // R mod p, R^2 mod p
+
+  Vec<N> mul(const Vec<N>& a, const Vec<N>& b) const {
+    Vec<N> r;
+    mont_mul_cios<N>(r.data(), a.data(), b.data(), M);
+    return r;
+  }
+  Vec<N> add(const Vec<N>& a, const Vec<N>& b) const {
+    Vec<N> r;
+    add_mod<N>(r.data(), a.data(), b.data(), M);
+    return r;
+  }
+  Vec<N> to_mont(const Vec<N>& a) const { return mul(a, r2); }
+  Vec<N> from_mont(const Vec<N>& a) const {
+    Vec<N> one{};
+    one[0] = 1;
+    return mul(a, one);
+  }
+  // base (Montgomery) ^ e, e given as 32-bit little-endian words
+  Vec<N> pow(const Vec<N>& base, const std::vector<uint32_t>& e) const {
+    Vec<N> acc = r1, b = base;
+    for (size_t i = 0; i < e.size() * 32; ++i) {
+      if ((e[i / 32] >> (i % 32)) & 1) acc = mul(acc, b);
+      b = mul(b, b);
+    }
+    return acc;
+  }
+  Vec<N> pow_u64(const Vec<N>& base, uint64_t e) const {
+    return pow(base, std::vector<uint32_t>{(uint32_t)e, (uint32_t)(e >> 32)});
+  }
+};
+
+template <int N>
+static bool vec_lt(const Vec<N>& a, const Vec<N>& b) {
+  for (int i = N - 1; i >= 0; --i)
+    if (a[i] != b[i]) return a[i] < b[i];
+  return false;
+}
+
+// ------------------------------------------------------------------------------ plan
+struct PlanBase {
+  virtual ~PlanBase() = default;
+  virtual int run(void* d, unsigned batch, bool inverse, hipStream_t st) = 0;
+  virtual int pointwise(const void* a, const void* b, void* c, hipStream_t st) = 0;
+  virtual int fill(void* d, int kind, uint64_t seed, hipStream_t st) = 0;
+  uint64_t n = 0;
+  unsigned log_n = 0, elem_bytes = 0, npass = 0;
+  unsigned r[8] = {0};
+  int device = 0;
+};
+
+// radices for log_n: near-equal split with each radix <= tile_log - 2 so that every global access
+// is a >= 4-element contiguous run (T = TILE / R >= 4).
+static void schedule(unsigned log_n, unsigned tile_log, unsigned* r, unsigned& p) {
+  if (log_n <= 2) { p = 0; return; }
+  if (log_n <= tile_log) { p = 1; r[0] = log_n; return; }
+  const unsigned rmax = tile_log - 2;
+  p = (log_n + rmax - 1) / rmax;
+  if (p < 2) p = 2;
+  const unsigned base = log_n / p, rem = log_n % p;
+  for (unsigned i = 0; i < p; ++i) r[i] = base + (i < rem ? 1 : 0);
+}
+
+template <int N, int MEMW>
+struct PlanImpl final : PlanBase {
+  HostField<N> H;
+  FieldArgs<N> Ff{}, Fi{};
+  Elem<N> ninv_m{}, r2_e{};
+  uint32_t* d_tab = nullptr;
+  uint32_t* d_scratch = nullptr;
+  size_t scratch_elems = 0;
+  // table word offsets
+  size_t off_int_f[8] = {0}, off_int_i[8] = {0};
+  size_t off_lo_f = 0, off_hi_f = 0, off_lo_i = 0, off_hi_i = 0, off_hi_is = 0;
+  unsigned lo_bits = 0;
+  uint32_t nrand = 1, top_bits = 28;
+
+  ~PlanImpl() override {
+    int cur = 0;
+    hipGetDevice(&cur);
+    hipSetDevice(device);
+    if (d_tab) hipFree(d_tab);
+    if (d_scratch) hipFree(d_scratch);
+    hipSetDevice(cur);
+  }
+
+  // modulus / generator as N 32-bit words
+  int init(const uint32_t* p, const uint32_t* g, unsigned log_n_, int dev) {
+    device = dev;
+    log_n = log_n_;
+    n = 1ull << log_n;
+    elem_bytes = 4 * MEMW;
+    // ---- modulus checks: odd, top word < 2^31 - 1 (no-carry Montgomery), p > 2
+    for (int i = 0; i < N; ++i) H.M.p[i] = p[i];
+    if (!(p[0] & 1)) return NTT_ERR_FIELD;
+    if (p[N - 1] >= 0x7fffffffu) return NTT_ERR_FIELD;
+    uint32_t inv = 1;
+    for (int i = 0; i < 5; ++i) inv *= 2 - p[0] * inv;
+    H.M.pinv = 0u - inv;
+    // R mod p, R^2 mod p by doubling
+    Vec<N> x{};
+    x[0] = 1;
+    for (int k = 0; k < 32 * N; ++k) x = H.add(x, x);
+    H.r1 = x;
+    for (int k = 0; k < 32 * N; ++k) x = H.add(x, x);
+    H.r2 = x;
+    Vec<N> pv;
+    for (int i = 0; i < N; ++i) pv[i] = p[i];
+    Vec<N> gv;
+    for (int i = 0; i < N; ++i) gv[i] = g[i];
+    if (!vec_lt<N>(gv, pv)) return NTT_ERR_FIELD;
+    // (p - 1) >> log_n, and n | p - 1
+    std::vector<uint32_t> pm1(p, p + N);
+    pm1[0] -= 1;  // p odd: no borrow
+    for (unsigned b = 0; b < log_n; ++b)
+      if ((pm1[b / 32] >> (b % 32)) & 1) return NTT_ERR_FIELD;
+    std::vector<uint32_t> e(N, 0);
+    for (int i = 0; i < N; ++i) {
+      const unsigned wsh = log_n / 32, bsh = log_n % 32;
+      uint64_t lo = (i + wsh < (unsigned)N) ? pm1[i + wsh] : 0;
+      uint64_t hi = (i + wsh + 1 < (unsigned)N) ? pm1[i + wsh + 1] : 0;
+      e[i] = (uint32_t)(((hi << 32) | lo) >> bsh);
+    }
+    const Vec<N> gm = H.to_mont(gv);
+    const Vec<N> w = H.pow(gm, e);  // w_n (Montgomery)
+    // primitive: w^(n/2) == -1 (n >= 2)
+    if (log_n >= 1) {
+      Vec<N> pm1v;
+      for (int i = 0; i < N; ++i) pm1v[i] = pm1[i];
+      const Vec<N> h = H.from_mont(H.pow_u64(w, n / 2));
+      if (h != pm1v) return NTT_ERR_FIELD;
+    }
+    std::vector<uint32_t> pm2(p, p + N);  // p - 2 with borrow (BLS12-381 Fr has p[0] = 1)
+    {
+      uint64_t br = 2;
+      for (int i = 0; i < N && br; ++i) {
+        const uint64_t d = (uint64_t)pm2[i] - br;
+        pm2[i] = (uint32_t)d;
+        br = (d >> 63) & 1;
+      }
+    }
+    const Vec<N> winv = H.pow(w, pm2);
+    Vec<N> nv{};
+    nv[0] = (uint32_t)n;
+    if (N > 1) nv[1] = (uint32_t)(n >> 32);
+    const Vec<N> ninv = H.pow(H.to_mont(nv), pm2);
+    for (int i = 0; i < N; ++i) {
+      ninv_m.w[i] = ninv[i];
+      r2_e.w[i] = H.r2[i];
+    }
+    // field args per direction
+    auto fill_args = [&](FieldArgs<N>& F, const Vec<N>& wn) {
+      F.M = H.M;
+      Vec<N> w8 = (log_n >= 3) ? H.pow_u64(wn, n / 8) : H.r1;
+      Vec<N> acc = w8;
+      for (int k = 0; k < 3; ++k) {
+        for (int i = 0; i < N; ++i) F.w8[k][i] = acc[i];
+        acc = H.mul(acc, w8);
+      }
+      for (int i = 0; i < N; ++i) F.one[i] = H.r1[i];
+    };
+    fill_args(Ff, w);
+    fill_args(Fi, winv);
+
+    // random-fill parameters: top nonzero 64-bit limb of p, masked to bitlen-1 bits
+    {
+      const int L64 = (N + 1) / 2;
+      int top = 0;
+      for (int i = L64 - 1; i >= 0; --i) {
+        const uint64_t limb = (uint64_t)p[2 * i] | ((2 * i + 1 < N) ? (uint64_t)p[2 * i + 1] << 32 : 0);
+        if (limb) { top = i; break; }
+      }
+      const uint64_t tl = (uint64_t)p[2 * top] | ((2 * top + 1 < N) ? (uint64_t)p[2 * top + 1] << 32 : 0);
+      nrand = top + 1;
+      top_bits = 63 - __builtin_clzll(tl);  // bitlen - 1
+    }
+
+    // ---- schedule + tables
+    schedule(log_n, tile_log(N), r, npass);
+    std::vector<uint32_t> host;
+    auto push_powers = [&](const Vec<N>& base, uint64_t count, const Vec<N>* scale) -> size_t {
+      const size_t off = host.size();
+      Vec<N> cur = scale ? *scale : H.r1;
+      for (uint64_t e2 = 0; e2 < count; ++e2) {
+        host.insert(host.end(), cur.begin(), cur.end());
+        cur = H.mul(cur, base);
+      }
+      // pad to 16 B
+      while (host.size() % 4) host.push_back(0);
+      return off;
+    };
+    const Vec<N> ninv_v = ninv;
+    for (int dir = 0; dir < 2; ++dir) {
+      const Vec<N>& wn = dir ? winv : w;
+      size_t* off_int = dir ? off_int_i : off_int_f;
+      if (npass == 0) {
+        off_int[0] = push_powers(wn, n, nullptr);
+      } else {
+        for (unsigned i = 0; i < npass; ++i) off_int[i] = push_powers(H.pow_u64(wn, n >> r[i]), 1ull << r[i], nullptr);
+      }
+      if (npass >= 2) {
+        lo_bits = (log_n + 1) / 2;
+        const size_t lo = push_powers(wn, 1ull << lo_bits, nullptr);
+        const Vec<N> step = H.pow_u64(wn, 1ull << lo_bits);
+        const size_t hi = push_powers(step, 1ull << (log_n - lo_bits), nullptr);
+        if (dir == 0) {
+          off_lo_f = lo;
+          off_hi_f = hi;
+        } else {
+          off_lo_i = lo;
+          off_hi_i = hi;
+          off_hi_is = push_powers(step, 1ull << (log_n - lo_bits), &ninv_v);
+        }
+      }
+    }
+    int cur = 0;
+    hipGetDevice(&cur);
+    if (hipSetDevice(device) != hipSuccess) return NTT_ERR_HIP;
+    int rc = NTT_OK;
+    if (hipMalloc(&d_tab, host.size() * 4) != hipSuccess ||
+        hipMemcpy(d_tab, host.data(), host.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+      rc = NTT_ERR_HIP;
+    if (rc == NTT_OK && npass >= 2) rc = ensure_scratch(1);
+    hipSetDevice(cur);
+    return rc;
+  }
+
+  int ensure_scratch(unsigned batch) {
+    const size_t need = (size_t)n * batch;
+    if (need <= scratch_elems) return NTT_OK;
+    if (d_scratch) hipFree(d_scratch);
+    d_scratch = nullptr;
+    scratch_elems = 0;
+    if (hipMalloc(&d_scratch, need * MEMW * 4) != hipSuccess) return NTT_ERR_HIP;
+    scratch_elems = need;
+    return NTT_OK;
+  }
+
+  PassArgs<N> base_args(bool inverse) const {
+    PassArgs<N> A;
+    memset(&A, 0, sizeof(A));
+    A.F = inverse ? Fi : Ff;
+    A.log_n = log_n;
+    A.lo_bits = lo_bits;
+    for (int i = 0; i < N; ++i) A.ninv[i] = ninv_m.w[i];
+    A.batch_stride = (size_t)n * MEMW;
+    return A;
+  }
+
+  int run(void* d, unsigned batch, bool inverse, hipStream_t st) override {
+    if (!d || batch == 0) return NTT_ERR_ARG;
+    if (log_n == 0) return NTT_OK;
+    uint32_t* data = static_cast<uint32_t*>(d);
+    const size_t* off_int = inverse ? off_int_i : off_int_f;
+    hipError_t e = hipSuccess;
+    if (npass == 0) {
+      PassArgs<N> A = base_args(inverse);
+      A.tw_int = d_tab + off_int[0];
+      A.flags = inverse ? 1u : 0u;
+      e = launch_naive<N, MEMW>(data, data, A, batch, st);
+    } else if (npass == 1) {
+      PassArgs<N> A = base_args(inverse);
+      A.tw_int = d_tab + off_int[0];
+      A.flags = inverse ? 1u : 0u;
+      e = launch_pass<N, MEMW>(KIND_SINGLE, (int)r[0], data, data, A, 1, batch, st);
+    } else {
+      if (int rc = ensure_scratch(batch)) return rc;
+      const uint32_t grid = (uint32_t)(n >> tile_log(N));
+      unsigned blk = log_n;
+      for (unsigned i = 0; i + 1 < npass && e == hipSuccess; ++i) {
+        PassArgs<N> A = base_args(inverse);
+        A.tw_int = d_tab + off_int[i];
+        A.tw_lo = d_tab + (inverse ? off_lo_i : off_lo_f);
+        A.tw_hi = d_tab + (inverse ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
+        A.log_blk = blk;
+        A.log_m = log_n - blk;
+        const uint32_t* src = (i == 0) ? data : d_scratch;
+        e = launch_pass<N, MEMW>(KIND_COLUMN, (int)r[i], src, d_scratch, A, grid, batch, st);
+        blk -= r[i];
+      }
+      if (e == hipSuccess) {
+        PassArgs<N> A = base_args(inverse);
+        A.tw_int = d_tab + off_int[npass - 1];
+        A.r1 = r[0];
+        A.nmid = npass - 2;
+        // middle digits k_2..k_{p-1}, least significant (k_{p-1}) first
+        for (unsigned m = 0; m < A.nmid; ++m) {
+          const unsigned idx = npass - 2 - m;  // pass index (0-based) of digit k_{idx+1}
+          A.mid_bits[m] = r[idx];
+          unsigned off = 0;
+          for (unsigned j = 1; j < idx; ++j) off += r[j];
+          A.mid_off[m] = off;
+        }
+        e = launch_pass<N, MEMW>(KIND_FINAL, (int)r[npass - 1], d_scratch, data, A, grid, batch, st);
+      }
+    }
+    return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+  }
+
+  int pointwise(const void* a, const void* b, void* c, hipStream_t st) override {
+    if (!a || !b || !c) return NTT_ERR_ARG;
+    hipError_t e = launch_pointwise<N, MEMW>(static_cast<const uint32_t*>(a), static_cast<const uint32_t*>(b),
+                                             static_cast<uint32_t*>(c), n, Ff, r2_e, st);
+    return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+  }
+
+  int fill(void* d, int kind, uint64_t seed, hipStream_t st) override {
+    if (!d || (kind != 0 && kind != 1)) return NTT_ERR_ARG;
+    hipError_t e = launch_fill<N, MEMW>(kind, static_cast<uint32_t*>(d), n, seed, nrand, top_bits, st);
+    return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+  }
+};
+
+// ------------------------------------------------------------------------------ built-in fields
+struct FieldDef {
+  uint64_t p[4];
+  uint64_t g;
+};
+static const FieldDef kFields[3] = {
+    {{469762049ull, 0, 0, 0}, 3},
+    {{0x43e1f593f0000001ull, 0x2833e84879b97091ull, 0xb85045b68181585dull, 0x30644e72e131a029ull}, 5},
+    {{0xffffffff00000001ull, 0x53bda402fffe5bfeull, 0x3339d80809a1d805ull, 0x73eda753299d7d48ull}, 7},
+};
+
+static int make_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, const uint64_t* g64, unsigned limbs64,
+                     unsigned log_n, int device) {
+  if (log_n > 40) return NTT_ERR_ARG;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return NTT_ERR_NODEV;
+  if (device < 0 || device >= ndev) return NTT_ERR_ARG;
+  uint32_t p32[12] = {0}, g32[12] = {0};
+  for (unsigned i = 0; i < limbs64; ++i) {
+    p32[2 * i] = (uint32_t)p64[i];
+    p32[2 * i + 1] = (uint32_t)(p64[i] >> 32);
+    g32[2 * i] = (uint32_t)g64[i];
+    g32[2 * i + 1] = (uint32_t)(g64[i] >> 32);
+  }
+  int rc;
+  if (limbs64 == 1) {
+    if (p64[0] >= (1ull << 31)) return NTT_ERR_FIELD;  // `long long` path: 31-bit primes
+    auto impl = std::make_unique<PlanImpl<1, 2>>();
+    rc = impl->init(p32, g32, log_n, device);
+    out = std::move(impl);
+  } else if (limbs64 == 4) {
+    auto impl = std::make_unique<PlanImpl<8, 8>>();
+    rc = impl->init(p32, g32, log_n, device);
+    out = std::move(impl);
+  } else if (limbs64 == 6) {
+    auto impl = std::make_unique<PlanImpl<12, 12>>();
+    rc = impl->init(p32, g32, log_n, device);
+    out = std::move(impl);
+  } else {
+    return NTT_ERR_ARG;
+  }
+  if (rc != NTT_OK) out.reset();
+  return rc;
+}
+
+static int set_err(int rc) {
+  g_last_error = rc;
+  return rc;
+}
+
+}  // namespace
+
+struct ntt_plan {
+  std::unique_ptr<PlanBase> impl;
+};
+
+extern "C" {
+
+int ntt_plan_create_custom(ntt_plan** out, const uint64_t* modulus, const uint64_t* generator, unsigned limbs64,
+                           unsigned log_n, int device) {
+  if (!out || !modulus || !generator) return set_err(NTT_ERR_ARG);
+  *out = nullptr;
+  std::unique_ptr<PlanBase> impl;
+  int rc = make_plan(impl, modulus, generator, limbs64, log_n, device);
+  if (rc != NTT_OK) return set_err(rc);
+  *out = new ntt_plan{std::move(impl)};
+  return set_err(NTT_OK);
+}
+
+int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device) {
+  if (field_id < 0 || field_id > 2) return set_err(NTT_ERR_ARG);
+  if (limbs64 == 1 && field_id != NTT_FIELD_P469762049) return set_err(NTT_ERR_ARG);
+  const FieldDef& F = kFields[field_id];
+  uint64_t p[6] = {0}, g[6] = {0};
+  const unsigned L = limbs64 > 6 ? 6 : limbs64;
+  for (unsigned i = 0; i < L && i < 4; ++i) p[i] = F.p[i];
+  g[0] = F.g;
+  return ntt_plan_create_custom(out, p, g, limbs64, log_n, device);
+}
+
+static int run_plan(ntt_plan* plan, void* d, unsigned batch, bool inv, void* stream) {
+  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
+  int cur = 0;
+  hipGetDevice(&cur);
+  if (cur != plan->impl->device) hipSetDevice(plan->impl->device);
+  int rc = plan->impl->run(d, batch, inv, static_cast<hipStream_t>(stream));
+  if (cur != plan->impl->device) hipSetDevice(cur);
+  return set_err(rc);
+}
+
+int ntt_forward(ntt_plan* plan, void* d_data, void* s) { return run_plan(plan, d_data, 1, false, s); }
+int ntt_inverse(ntt_plan* plan, void* d_data, void* s) { return run_plan(plan, d_data, 1, true, s); }
+int ntt_forward_batch(ntt_plan* plan, void* d_data, unsigned b, void* s) { return run_plan(plan, d_data, b, false, s); }
+int ntt_inverse_batch(ntt_plan* plan, void* d_data, unsigned b, void* s) { return run_plan(plan, d_data, b, true, s); }
+
+int ntt_pointwise_mul(ntt_plan* plan, const void* a, const void* b, void* c, void* s) {
+  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
+  return set_err(plan->impl->pointwise(a, b, c, static_cast<hipStream_t>(s)));
+}
+
+int ntt_polymul(ntt_plan* plan, void* a, void* b, void* c, void* s) {
+  int rc = ntt_forward(plan, a, s);
+  if (rc == NTT_OK) rc = ntt_forward(plan, b, s);
+  if (rc == NTT_OK) rc = ntt_pointwise_mul(plan, a, b, c, s);
+  if (rc == NTT_OK) rc = ntt_inverse(plan, c, s);
+  return set_err(rc);
+}
+
+int ntt_fill(ntt_plan* plan, void* d, int kind, uint64_t seed, void* s) {
+  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
+  return set_err(plan->impl->fill(d, kind, seed, static_cast<hipStream_t>(s)));
+}
+
+int ntt_plan_info(const ntt_plan* plan, uint64_t* n, unsigned* elem_bytes, unsigned* npasses, unsigned radix_log[8]) {
+  if (!plan || !plan->impl) return NTT_ERR_ARG;
+  const PlanBase& P = *plan->impl;
+  if (n) *n = P.n;
+  if (elem_bytes) *elem_bytes = P.elem_bytes;
+  if (npasses) *npasses = P.npass;
+  if (radix_log)
+    for (int i = 0; i < 8; ++i) radix_log[i] = P.r[i];
+  return NTT_OK;
+}
+
+int ntt_plan_destroy(ntt_plan* plan) {
+  delete plan;
+  return NTT_OK;
+}
+
+const char* ntt_strerror(int status) {
+  switch (status) {
+    case NTT_OK: return "ok";
+    case NTT_ERR_ARG: return "invalid argument";
+    case NTT_ERR_HIP: return "HIP runtime error";
+    case NTT_ERR_RCCL: return "RCCL error";
+    case NTT_ERR_FIELD: return "unsupported modulus or no root of unity of this order";
+    case NTT_ERR_NODEV: return "no HIP device";
+    default: return "unknown status";
+  }
+}
+
+int ntt_last_error(void) { return g_last_error; }
+
+// ---------------------------------------------------------------- reference-shaped shims
+// Plans are cached per (modulus, generator, limbs, log_n, device) like a persistent version of the
+// reference drivers' per-call table setup.
+static std::mutex g_cache_mu;
+static std::map<std::tuple<std::vector<uint64_t>, std::vector<uint64_t>, unsigned, unsigned, int>,
+                std::unique_ptr<ntt_plan>>
+    g_cache;
+
+static ntt_plan* cached_plan(const uint64_t* p, const uint64_t* g, unsigned limbs64, unsigned log_n, int* rc) {
+  int dev = 0;
+  hipGetDevice(&dev);
+  auto key = std::make_tuple(std::vector<uint64_t>(p, p + limbs64), std::vector<uint64_t>(g, g + limbs64), limbs64,
+                             log_n, dev);
+  std::lock_guard<std::mutex> lk(g_cache_mu);
+  auto it = g_cache.find(key);
+  if (it != g_cache.end()) {
+    *rc = NTT_OK;
+    return it->second.get();
+  }
+  ntt_plan* pl = nullptr;
+  *rc = ntt_plan_create_custom(&pl, p, g, limbs64, log_n, dev);
+  if (*rc != NTT_OK) return nullptr;
+  g_cache[key].reset(pl);
+  return pl;
+}
+
+static int blocking_forward(ntt_plan* pl, void* d) {
+  int rc = ntt_forward(pl, d, nullptr);
+  if (rc == NTT_OK && hipDeviceSynchronize() != hipSuccess) rc = NTT_ERR_HIP;
+  return set_err(rc);
+}
+
+void SSIP(long long* x, long long omega, unsigned log_n) {
+  const uint64_t p = 469762049ull, g = (uint64_t)omega;
+  int rc = NTT_OK;
+  ntt_plan* pl = cached_plan(&p, &g, 1, log_n, &rc);
+  if (!pl) { set_err(rc); return; }
+  blocking_forward(pl, x);
+}
+
+int NTT_GZKP_64(long long* data, const void* /*reverse*/, long long len, long long omega, int /*B*/, int /*G*/,
+                long long /*reverse_num*/) {
+  if (len <= 0 || (len & (len - 1))) return set_err(NTT_ERR_ARG);
+  const unsigned log_n = (unsigned)__builtin_ctzll((unsigned long long)len);
+  const uint64_t p = 469762049ull, g = (uint64_t)omega;
+  int rc = NTT_OK;
+  ntt_plan* pl = cached_plan(&p, &g, 1, log_n, &rc);
+  if (!pl) return set_err(rc);
+  return blocking_forward(pl, data);
+}
+
+int NTT_GZKP_256(uint32_t* data, uint32_t len, const void* /*reverse*/, uint32_t /*reverse_len*/,
+                 const uint32_t prime[8], const uint32_t omega[8], uint32_t /*B*/, uint32_t /*G*/) {
+  if (!data || !prime || !omega || len == 0 || (len & (len - 1))) return set_err(NTT_ERR_ARG);
+  const unsigned log_n = (unsigned)__builtin_ctz(len);
+  uint64_t p[4], g[4];
+  for (int i = 0; i < 4; ++i) {
+    p[i] = (uint64_t)prime[2 * i] | ((uint64_t)prime[2 * i + 1] << 32);
+    g[i] = (uint64_t)omega[2 * i] | ((uint64_t)omega[2 * i + 1] << 32);
+  }
+  int rc = NTT_OK;
+  ntt_plan* pl = cached_plan(p, g, 4, log_n, &rc);
+  if (!pl) return set_err(rc);
+  return blocking_forward(pl, data);
+}
+
+}  // extern "C"

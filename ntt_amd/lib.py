@@ -1,0 +1,98 @@
+"""ctypes binding of libntt.so (include/ntt.h).
+
+The library is the product: there is no CPU fallback.  ``load()`` raises if the in-tree
+``ntt_amd/libntt.so`` is missing (build it with ``python -m ntt_amd.build`` or
+``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libntt.so")
+
+NTT_OK = 0
+NTT_FIELD_P469762049 = 0
+NTT_FIELD_BN254_FR = 1
+NTT_FIELD_BLS12_381_FR = 2
+
+# Every symbol declared in include/ntt.h with its ctypes prototype: (restype, argtypes).
+_vp = C.c_void_p
+PROTOTYPES = {
+    "ntt_plan_create": (C.c_int, [C.POINTER(_vp), C.c_int, C.c_uint, C.c_uint, C.c_int]),
+    "ntt_plan_create_custom": (C.c_int, [C.POINTER(_vp), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_uint,
+                                         C.c_uint, C.c_int]),
+    "ntt_forward": (C.c_int, [_vp, _vp, _vp]),
+    "ntt_inverse": (C.c_int, [_vp, _vp, _vp]),
+    "ntt_forward_batch": (C.c_int, [_vp, _vp, C.c_uint, _vp]),
+    "ntt_inverse_batch": (C.c_int, [_vp, _vp, C.c_uint, _vp]),
+    "ntt_pointwise_mul": (C.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "ntt_polymul": (C.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "ntt_fill": (C.c_int, [_vp, _vp, C.c_int, C.c_uint64, _vp]),
+    "ntt_plan_info": (C.c_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint), C.POINTER(C.c_uint),
+                                C.POINTER(C.c_uint)]),
+    "ntt_plan_destroy": (C.c_int, [_vp]),
+    "ntt_strerror": (C.c_char_p, [C.c_int]),
+    "SSIP": (None, [_vp, C.c_longlong, C.c_uint]),
+    "NTT_GZKP_256": (C.c_int, [_vp, C.c_uint32, _vp, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                               C.c_uint32, C.c_uint32]),
+    "NTT_GZKP_64": (C.c_int, [_vp, _vp, C.c_longlong, C.c_longlong, C.c_int, C.c_int, C.c_longlong]),
+    "ntt_last_error": (C.c_int, []),
+    # multi-GPU (include/ntt_dist.h)
+    "ntt_dist_unique_id": (C.c_int, [C.c_char_p]),
+    "ntt_dist_comm_create": (C.c_int, [C.POINTER(_vp), C.c_char_p, C.c_int, C.c_int, C.c_int]),
+    "ntt_dist_comm_destroy": (C.c_int, [_vp]),
+    "ntt_dist_plan_create": (C.c_int, [C.POINTER(_vp), _vp, C.c_int, C.c_uint, C.c_uint]),
+    "ntt_dist_forward": (C.c_int, [_vp, _vp, _vp]),
+    "ntt_dist_inverse": (C.c_int, [_vp, _vp, _vp]),
+    "ntt_dist_pointwise_mul": (C.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "ntt_dist_info": (C.c_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint),
+                                C.POINTER(C.c_uint)]),
+    "ntt_dist_fill": (C.c_int, [_vp, _vp, C.c_int, C.c_uint64, _vp]),
+    "ntt_dist_plan_destroy": (C.c_int, [_vp]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class NTTError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        msg = _strerror(status)
+        super().__init__(f"{what}: {msg} (status {status})" if what else f"{msg} (status {status})")
+        self.status = status
+
+
+def _strerror(status: int) -> str:
+    try:
+        return load().ntt_strerror(status).decode()
+    except Exception:  # pragma: no cover - library unavailable
+        return "error"
+
+
+def load(path: str = LIB_PATH) -> C.CDLL:
+    """Load libntt.so (in-tree) and attach prototypes.  Raises if it is missing."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise FileNotFoundError(
+                f"{path} not found: build the HIP extension first (python -m ntt_amd.build); "
+                "the NTT has no CPU fallback")
+        lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in PROTOTYPES.items():
+            fn = getattr(lib, name, None)
+            if fn is None:
+                continue
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def check(status: int, what: str = "") -> None:
+    if status != NTT_OK:
+        raise NTTError(status, what)
