@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""Benchmark: field-elements/sec of a 2^24-point forward NTT over BN254 Fr (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+A "step" is one forward transform of the whole 2^24-element vector (SURVEY §8d synthetic vector B,
+SplitMix64 limbs), resident in HBM when the timed region starts.  N = 1: one MI355X
+(BASELINE configs[1]-class single-GPU workload at the headline size).  N > 1 (launched by
+torch.distributed.run, one rank per GPU): the SAME 2^24 transform distributed over N GPUs as a
+four-step with one RCCL all-to-all (strong scaling); `value` is always the whole-job
+rate n / t.
+
+Rank 0 prints one JSON line with `roofline` (HBM roofline of the dominant kernel, measured with
+HIP events on its launch stream inside the timed region) and `cpu_baseline` (the C oracle on the
+host, a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = "field-elements/sec, 2^24 forward NTT over BN254 Fr; achieved HBM GB/s vs peak"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+FIELD_NAMES = {0: "P469762049", 1: "BN254_FR", 2: "BLS12_381_FR"}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--log-n", type=int, default=24)
+    ap.add_argument("--field", type=int, default=1)
+    ap.add_argument("--limbs", type=int, default=4)
+    ap.add_argument("--inverse", action="store_true", help="time the inverse instead of the forward")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-log-n", type=int, default=22, help="C-oracle sample size (log2)")
+    return ap.parse_args()
+
+
+def cpu_baseline(field_id: int, limbs: int, log_n: int):
+    """The C oracle (oracle/ntt_oracle.c, a restatement of GZKP-NTT.cu:30-48) on the host, 1 core."""
+    from oracle import oracle_c as OC
+    from oracle import ntt_ref as R
+    p, g = R.FIELDS[field_id]
+    x = OC.random_limbs(field_id, 1 << log_n, seed=2, L=limbs)
+    t0 = time.perf_counter()
+    OC.ntt_mp(x, p, g)
+    dt = time.perf_counter() - t0
+    return {"value": (1 << log_n) / dt, "unit": "field-elements/s", "cores": 1, "kind": "port",
+            "sample": f"one 2^{log_n}-point forward NTT ({FIELD_NAMES[field_id]}, {limbs}x64-bit limbs, SplitMix64 "
+                      f"input) by the C oracle on 1 host core ({platform.processor() or platform.machine()}, "
+                      f"os.cpu_count()={os.cpu_count()}): {dt:.2f} s; the n log n cost makes the 2^24 rate "
+                      f"~{log_n}/24 of this",
+            "seconds": dt}
+
+
+def load_traffic(tag: str):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary for this workload (or None)."""
+    path = os.path.join(HERE, "profiles", "pmc_summary.json")
+    try:
+        d = json.load(open(path))
+        return d.get(tag)
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    n = 1 << args.log_n
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        from ntt_amd.distributed import DistNTT
+        eng = DistNTT(field_id=args.field, log_n=args.log_n, limbs64=args.limbs, device=local)
+        data = eng.empty()
+        eng.fill(data, "random", seed=2)
+        step = (lambda: eng.inverse(data)) if args.inverse else (lambda: eng.forward(data))
+        plan_for_prof = eng
+    else:
+        from ntt_amd.ntt import NTTPlan
+        plan = NTTPlan(field_id=args.field, log_n=args.log_n, limbs64=args.limbs, device=local)
+        data = plan.empty()
+        plan.fill(data, "random", seed=2)
+        step = (lambda: plan.inverse(data)) if args.inverse else (lambda: plan.forward(data))
+        plan_for_prof = plan
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # ---- timed region: K steps bracketed by barrier + synchronize; per-launch HIP events recorded
+    # on the launch stream between kernels (ntt_plan_set_profiling) accumulate per-launch times.
+    plan_for_prof.set_profiling(True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    launch_avg = plan_for_prof.last_launch_ms()  # per-launch average over the timed steps (<= 64)
+    plan_for_prof.set_profiling(False)
+
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = n / (elapsed / args.steps)
+
+    elem_bytes = 8 if args.limbs == 1 else 8 * args.limbs
+    passes = list(getattr(plan_for_prof, "passes", []))
+    out = {
+        "metric": METRIC if (args.field == 1 and args.log_n == 24 and not args.inverse) else
+        f"field-elements/sec, 2^{args.log_n} {'inverse' if args.inverse else 'forward'} NTT over "
+        f"{FIELD_NAMES[args.field]}",
+        "value": value,
+        "unit": "field-elements/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "uint256 (8x32-bit limbs, Montgomery)" if args.limbs == 4 else
+                 ("uint384 (12x32-bit limbs, Montgomery)" if args.limbs == 6 else "uint32 Montgomery"),
+        "data": "synthetic: SplitMix64 field elements (SURVEY §8d vector B, seed 2), resident in HBM",
+        "config": {"workload": f"2^{args.log_n}-point {'inverse' if args.inverse else 'forward'} NTT, "
+                               f"{FIELD_NAMES[args.field]}, {args.limbs}x64-bit limbs, natural order, in place",
+                   "log_n": args.log_n, "field": FIELD_NAMES[args.field], "limbs64": args.limbs,
+                   "passes_log_radix": passes,
+                   "parallelism": "single GPU" if world == 1 else f"four-step over {world} GPUs (RCCL all-to-all)"},
+    }
+    if launch_avg:
+        # dominant kernel = the longest launch; algorithmic bytes per launch = one read + one write
+        # of the local vector (2*n*S per pass over all n elements).
+        k = max(range(len(launch_avg)), key=lambda i: launch_avg[i])
+        local_n = n // world
+        alg_bytes = 2 * local_n * elem_bytes
+        achieved = alg_bytes / (launch_avg[k] * 1e-3) / 1e9
+        tag = f"f{args.field}_L{args.limbs}_n{args.log_n}_w{world}"
+        traffic = load_traffic(tag)
+        out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                           "frac": achieved / HBM_PEAK_GBPS,
+                           "traffic": traffic[k] if isinstance(traffic, list) and k < len(traffic) else None,
+                           "kernel": f"launch {k} of {len(launch_avg)}", "kernel_ms": launch_avg[k],
+                           "algorithmic_bytes_per_launch": alg_bytes,
+                           "launch_ms": launch_avg}
+        total_alg = 2 * n * elem_bytes * max(1, len(launch_avg))
+        out["hbm_effective_gbps_whole_transform"] = total_alg / world / (ms_per_step * 1e-3) / 1e9
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args.field, args.limbs if args.limbs != 1 else 1, args.cpu_log_n)
+        except Exception as e:  # pragma: no cover
+            out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

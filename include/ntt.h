@@ -78,6 +78,13 @@ int ntt_polymul(ntt_plan* plan, void* d_a, void* d_b, void* d_c, void* hip_strea
  * input, GZKP-NTT.cu:1587), kind 1 = SplitMix64 limbs with the top limb masked (seeded). */
 int ntt_fill(ntt_plan* plan, void* d_data, int kind, uint64_t seed, void* hip_stream);
 
+/* Per-launch timing for benchmarks: when enabled, every transform records HIP events on its
+ * stream between its kernel launches (a ring of 64 transforms, no host synchronisation);
+ * ntt_plan_last_launch_ms returns per-launch durations (ms) averaged over the transforms recorded
+ * since profiling was enabled (the last 64 at most), waiting for the most recent one. */
+int ntt_plan_set_profiling(ntt_plan* plan, int enable);
+int ntt_plan_last_launch_ms(ntt_plan* plan, float* ms, unsigned max_launches, unsigned* nlaunches);
+
 /* Plan introspection: n, bytes per element, number of passes and their log2 radices. */
 int ntt_plan_info(const ntt_plan* plan, uint64_t* n, unsigned* elem_bytes, unsigned* npasses, unsigned radix_log[8]);
 int ntt_plan_destroy(ntt_plan* plan);

@@ -85,6 +85,22 @@ struct PlanBase {
   unsigned log_n = 0, elem_bytes = 0, npass = 0;
   unsigned r[8] = {0};
   int device = 0;
+  // optional per-launch timing: events recorded on the caller's stream between launches, one
+  // slot per transform in a ring of kSlots transforms (no host synchronisation per transform)
+  static constexpr unsigned kSlots = 64, kEv = 9;
+  bool profiling = false;
+  hipEvent_t ev[kSlots][kEv] = {};
+  unsigned ev_used = 0, slot = 0, nrec = 0;
+  void begin(hipStream_t st) {
+    if (!profiling) return;
+    slot = nrec % kSlots;
+    ev_used = 0;
+    ++nrec;
+    mark(st);
+  }
+  void mark(hipStream_t st) {
+    if (profiling && ev_used < kEv) hipEventRecord(ev[slot][ev_used++], st);
+  }
 };
 
 // radices for log_n: near-equal split with each radix <= tile_log - 2 so that every global access
@@ -119,6 +135,9 @@ struct PlanImpl final : PlanBase {
     hipSetDevice(device);
     if (d_tab) hipFree(d_tab);
     if (d_scratch) hipFree(d_scratch);
+    for (auto& row : ev)
+      for (auto& e : row)
+        if (e) hipEventDestroy(e);
     hipSetDevice(cur);
   }
 
@@ -291,16 +310,19 @@ struct PlanImpl final : PlanBase {
     uint32_t* data = static_cast<uint32_t*>(d);
     const size_t* off_int = inverse ? off_int_i : off_int_f;
     hipError_t e = hipSuccess;
+    begin(st);
     if (npass == 0) {
       PassArgs<N> A = base_args(inverse);
       A.tw_int = d_tab + off_int[0];
       A.flags = inverse ? 1u : 0u;
       e = launch_naive<N, MEMW>(data, data, A, batch, st);
+      mark(st);
     } else if (npass == 1) {
       PassArgs<N> A = base_args(inverse);
       A.tw_int = d_tab + off_int[0];
       A.flags = inverse ? 1u : 0u;
       e = launch_pass<N, MEMW>(KIND_SINGLE, (int)r[0], data, data, A, 1, batch, st);
+      mark(st);
     } else {
       if (int rc = ensure_scratch(batch)) return rc;
       const uint32_t grid = (uint32_t)(n >> tile_log(N));
@@ -314,6 +336,7 @@ struct PlanImpl final : PlanBase {
         A.log_m = log_n - blk;
         const uint32_t* src = (i == 0) ? data : d_scratch;
         e = launch_pass<N, MEMW>(KIND_COLUMN, (int)r[i], src, d_scratch, A, grid, batch, st);
+        mark(st);
         blk -= r[i];
       }
       if (e == hipSuccess) {
@@ -330,6 +353,7 @@ struct PlanImpl final : PlanBase {
           A.mid_off[m] = off;
         }
         e = launch_pass<N, MEMW>(KIND_FINAL, (int)r[npass - 1], d_scratch, data, A, grid, batch, st);
+        mark(st);
       }
     }
     return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
@@ -471,6 +495,45 @@ int ntt_plan_info(const ntt_plan* plan, uint64_t* n, unsigned* elem_bytes, unsig
   if (radix_log)
     for (int i = 0; i < 8; ++i) radix_log[i] = P.r[i];
   return NTT_OK;
+}
+
+int ntt_plan_set_profiling(ntt_plan* plan, int enable) {
+  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
+  PlanBase& P = *plan->impl;
+  if (enable && !P.ev[0][0]) {
+    int cur = 0;
+    hipGetDevice(&cur);
+    hipSetDevice(P.device);
+    for (auto& row : P.ev)
+      for (auto& e : row)
+        if (hipEventCreate(&e) != hipSuccess) { hipSetDevice(cur); return set_err(NTT_ERR_HIP); }
+    hipSetDevice(cur);
+  }
+  P.profiling = enable != 0;
+  P.nrec = 0;
+  return set_err(NTT_OK);
+}
+
+// Average per-launch durations over the transforms recorded since profiling was enabled (at most
+// the last 64); waits for the most recent one.
+int ntt_plan_last_launch_ms(ntt_plan* plan, float* ms, unsigned max_launches, unsigned* nlaunches) {
+  if (!plan || !plan->impl || !ms) return set_err(NTT_ERR_ARG);
+  PlanBase& P = *plan->impl;
+  const unsigned k = P.ev_used ? P.ev_used - 1 : 0;
+  if (nlaunches) *nlaunches = k;
+  if (k == 0 || P.nrec == 0) return set_err(NTT_OK);
+  if (hipEventSynchronize(P.ev[P.slot][k]) != hipSuccess) return set_err(NTT_ERR_HIP);
+  const unsigned nslots = P.nrec < PlanBase::kSlots ? P.nrec : PlanBase::kSlots;
+  for (unsigned i = 0; i < k && i < max_launches; ++i) {
+    double acc = 0;
+    for (unsigned sl = 0; sl < nslots; ++sl) {
+      float t = 0;
+      if (hipEventElapsedTime(&t, P.ev[sl][i], P.ev[sl][i + 1]) != hipSuccess) return set_err(NTT_ERR_HIP);
+      acc += t;
+    }
+    ms[i] = (float)(acc / nslots);
+  }
+  return set_err(NTT_OK);
 }
 
 int ntt_plan_destroy(ntt_plan* plan) {

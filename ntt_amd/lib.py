@@ -34,6 +34,8 @@ PROTOTYPES = {
     "ntt_plan_info": (C.c_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint), C.POINTER(C.c_uint),
                                 C.POINTER(C.c_uint)]),
     "ntt_plan_destroy": (C.c_int, [_vp]),
+    "ntt_plan_set_profiling": (C.c_int, [_vp, C.c_int]),
+    "ntt_plan_last_launch_ms": (C.c_int, [_vp, C.POINTER(C.c_float), C.c_uint, C.POINTER(C.c_uint)]),
     "ntt_strerror": (C.c_char_p, [C.c_int]),
     "SSIP": (None, [_vp, C.c_longlong, C.c_uint]),
     "NTT_GZKP_256": (C.c_int, [_vp, C.c_uint32, _vp, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),

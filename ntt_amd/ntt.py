@@ -169,6 +169,16 @@ class NTTPlan:
                  "ntt_fill")
         return t
 
+    def set_profiling(self, enable: bool = True) -> None:
+        _L.check(self._lib.ntt_plan_set_profiling(self._h, int(bool(enable))), "ntt_plan_set_profiling")
+
+    def last_launch_ms(self) -> List[float]:
+        """Kernel durations (ms, HIP events on the launch stream) of the most recent transform."""
+        buf = (C.c_float * 16)()
+        k = C.c_uint()
+        _L.check(self._lib.ntt_plan_last_launch_ms(self._h, buf, 16, C.byref(k)), "ntt_plan_last_launch_ms")
+        return [buf[i] for i in range(k.value)]
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             self._lib.ntt_plan_destroy(self._h)
