@@ -1,0 +1,144 @@
+// Radix-2^29 prime-field engine for the 256-bit (L = 9) and 384-bit (L = 14) element classes.
+//
+// Why 29-bit limbs on gfx950: the only wide multiplier is v_mad_u64_u32 (32x32+64 -> 64, measured
+// 4.65 cycles per wave64 instruction, the same issue cost as a 32-bit carry add).  With 29-bit
+// limbs a column of the Montgomery product sums at most 2L products of < 2^58 (2L <= 28), which
+// never overflows the 64-bit accumulator: every partial product is exactly ONE v_mad_u64_u32 with
+// no carry handling, no zero-extension moves and no asm (162 MADs for L = 9, versus 128 MAD + 128
+// carry-add + moves for 8 x 32-bit limbs).  See DESIGN.md "Field arithmetic".
+//
+// Value invariant between operations: limbs normalised (< 2^29), value < 2p ("lazy" residues);
+// canonical (< p) only in HBM.  R = 2^(29L) > 16p for every supported field (p < 2^255), so a
+// Montgomery product of x < 8p by a canonical twiddle is < 2p.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#include <hip/hip_runtime.h>
+#define F29_HD __host__ __device__ __forceinline__
+#else
+#define F29_HD static inline
+#endif
+
+namespace ntt {
+
+constexpr uint32_t kMask29 = (1u << 29) - 1;
+
+template <int L>
+struct Mod29 {
+  uint32_t p[L];    // modulus, normalised 29-bit limbs
+  uint32_t p2[L];   // 2p, normalised
+  uint32_t pinv;    // -p^-1 mod 2^29
+};
+
+// unsigned carry normalisation: limbs may exceed 2^29 (non-negative); top limb keeps the excess
+template <int L>
+F29_HD void norm_u(uint32_t (&x)[L]) {
+#pragma unroll
+  for (int i = 0; i + 1 < L; ++i) {
+    x[i + 1] += x[i] >> 29;
+    x[i] &= kMask29;
+  }
+}
+// signed carry normalisation: limbs hold int32 values; returns the (signed) top limb
+template <int L>
+F29_HD int32_t norm_s(uint32_t (&x)[L]) {
+#pragma unroll
+  for (int i = 0; i + 1 < L; ++i) {
+    x[i + 1] = (uint32_t)((int32_t)x[i + 1] + ((int32_t)x[i] >> 29));
+    x[i] &= kMask29;
+  }
+  return (int32_t)x[L - 1];
+}
+
+// x -= q if x >= q (x, q normalised, x < 2q)
+template <int L>
+F29_HD void cond_sub(uint32_t (&x)[L], const uint32_t (&q)[L]) {
+  uint32_t t[L];
+#pragma unroll
+  for (int i = 0; i < L; ++i) t[i] = x[i] - q[i];
+  const bool neg = norm_s<L>(t) < 0;
+#pragma unroll
+  for (int i = 0; i < L; ++i) x[i] = neg ? x[i] : t[i];
+}
+
+// u = a + b mod-lazy: < 2p for a, b < 2p
+template <int L>
+F29_HD void add29(uint32_t (&u)[L], const uint32_t (&a)[L], const uint32_t (&b)[L], const Mod29<L>& M) {
+#pragma unroll
+  for (int i = 0; i < L; ++i) u[i] = a[i] + b[i];
+  norm_u<L>(u);
+  cond_sub<L>(u, M.p2);
+}
+// d = a - b + 2p (normalised, < 4p) for a, b < 2p
+template <int L>
+F29_HD void sub29_raw(uint32_t (&d)[L], const uint32_t (&a)[L], const uint32_t (&b)[L], const Mod29<L>& M) {
+#pragma unroll
+  for (int i = 0; i < L; ++i) d[i] = a[i] - b[i] + M.p2[i];
+  norm_s<L>(d);
+}
+// d = a - b lazily reduced: < 2p
+template <int L>
+F29_HD void sub29(uint32_t (&d)[L], const uint32_t (&a)[L], const uint32_t (&b)[L], const Mod29<L>& M) {
+  sub29_raw<L>(d, a, b, M);
+  cond_sub<L>(d, M.p2);
+}
+
+// Montgomery product r = a * b * 2^(-29L) mod p (finely-integrated product scanning).
+// a: normalised limbs, value < 8p; b: normalised, < p (twiddle) or < 2p.  r: normalised, < 2p.
+// Column bound: <= 2L products of < 2^58 plus the carried column (< 2^36): < 2^63 for L <= 14.
+template <int L>
+F29_HD void mont29(uint32_t (&r)[L], const uint32_t (&a)[L], const uint32_t (&b)[L], const Mod29<L>& M) {
+  uint32_t m[L];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+#pragma unroll
+    for (int j = 0; j < i; ++j) {
+      acc += (uint64_t)a[j] * b[i - j];
+      acc += (uint64_t)m[j] * M.p[i - j];
+    }
+    acc += (uint64_t)a[i] * b[0];
+    m[i] = ((uint32_t)acc * M.pinv) & kMask29;
+    acc += (uint64_t)m[i] * M.p[0];
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int i = L; i < 2 * L; ++i) {
+#pragma unroll
+    for (int j = i - L + 1; j < L; ++j) {
+      acc += (uint64_t)a[j] * b[i - j];
+      acc += (uint64_t)m[j] * M.p[i - j];
+    }
+    r[i - L] = (uint32_t)acc & kMask29;
+    acc >>= 29;
+  }
+}
+
+// ---------------------------------------------------------------- 32-bit <-> 29-bit limb packing
+// canonical little-endian 32-bit words (W32 of them) -> L normalised 29-bit limbs
+template <int L, int W32>
+F29_HD void pack29(uint32_t (&x)[L], const uint32_t (&w)[W32]) {
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const int bit = 29 * i, k = bit / 32, s = bit % 32;
+    const uint32_t lo = (k < W32) ? w[k] : 0u;
+    const uint32_t hi = (k + 1 < W32) ? w[k + 1] : 0u;
+    const uint64_t v = ((uint64_t)hi << 32) | lo;
+    x[i] = (uint32_t)(v >> s) & kMask29;
+  }
+}
+// L normalised 29-bit limbs -> W32 little-endian 32-bit words (value must fit 32*W32 bits)
+template <int L, int W32>
+F29_HD void unpack29(uint32_t (&w)[W32], const uint32_t (&x)[L]) {
+#pragma unroll
+  for (int k = 0; k < W32; ++k) {
+    const int bit = 32 * k, i = bit / 29, s = bit % 29;
+    uint32_t v = (i < L) ? (x[i] >> s) : 0u;
+    if (i + 1 < L) v |= x[i + 1] << (29 - s);
+    if (i + 2 < L && 58 - s < 32) v |= x[i + 2] << (58 - s);
+    w[k] = v;
+  }
+}
+
+}  // namespace ntt

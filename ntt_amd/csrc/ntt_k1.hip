@@ -1,5 +1,5 @@
-// Explicit instantiation of the NTT kernels for 1 x 32-bit limbs (2 words per element).
+// Explicit instantiation of the NTT kernels for the EngP engine.
 #include "ntt_kernels_impl.hpp"
 namespace ntt {
-NTT_INSTANTIATE(1, 2)
+NTT_INSTANTIATE(EngP)
 }  // namespace ntt

@@ -1,5 +1,5 @@
-// Explicit instantiation of the NTT kernels for 12 x 32-bit limbs (12 words per element).
+// Explicit instantiation of the NTT kernels for the Eng384 engine.
 #include "ntt_kernels_impl.hpp"
 namespace ntt {
-NTT_INSTANTIATE(12, 12)
+NTT_INSTANTIATE(Eng384)
 }  // namespace ntt

@@ -1,5 +1,5 @@
-// Explicit instantiation of the NTT kernels for 8 x 32-bit limbs (8 words per element).
+// Explicit instantiation of the NTT kernels for the Eng256 engine.
 #include "ntt_kernels_impl.hpp"
 namespace ntt {
-NTT_INSTANTIATE(8, 8)
+NTT_INSTANTIATE(Eng256)
 }  // namespace ntt

@@ -2,23 +2,28 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include "ntt_device.hpp"
+#include "engines.hpp"
 
 namespace ntt {
 
 enum : int { KIND_COLUMN = 0, KIND_FINAL = 1, KIND_SINGLE = 2 };
 
-// Elements per workgroup tile: 2048 x 32 B = 64 KiB of LDS (two workgroups per CU); the 384-bit
-// template halves the tile to keep the same LDS footprint.
-__host__ __device__ constexpr int tile_elems(int N) { return N >= 12 ? 1024 : 2048; }
-__host__ __device__ constexpr int tile_log(int N) { return N >= 12 ? 10 : 11; }
+// Elements per workgroup tile: 2048 for <= 9-word elements (72 KiB LDS for the 29-bit 256-bit
+// class: two workgroups per CU), 1024 for the 384-bit class.
+__host__ __device__ constexpr int tile_log_w(int ldsw) { return ldsw <= 9 ? 11 : 10; }
+__host__ __device__ constexpr int tile_elems_w(int ldsw) { return 1 << tile_log_w(ldsw); }
 
-template <int N>
+using Eng256 = Eng29<9, 8>;    // 4 x 64-bit limbs in HBM
+using Eng384 = Eng29<14, 12>;  // 6 x 64-bit limbs in HBM
+using EngP = Eng32<1, 2>;      // P469762049, `long long` in HBM
+
+template <class E>
 struct PassArgs {
-  FieldArgs<N> F;
-  const uint32_t* tw_int;  // w_R^e, e < R (this pass's radix), Montgomery form
+  typename E::Args F;
+  const uint32_t* tw_int;  // w_R^e, e < R (this pass's radix), engine table format
   const uint32_t* tw_lo;   // outer twiddles w_n^e = tw_lo[e mod 2^lo_bits] * tw_hi[e >> lo_bits]
   const uint32_t* tw_hi;
+  const uint32_t* tw_full;  // column pass: per-pass outer twiddle table (HBM element format) or null
   uint32_t lo_bits;
   uint32_t log_n;
   uint32_t log_blk;  // column pass: log2 of the block length N_i
@@ -28,20 +33,23 @@ struct PassArgs {
   uint32_t mid_bits[4];  // final pass: middle digit widths, least significant (k_{p-1}) first
   uint32_t mid_off[4];   // final pass: output bit offset (relative to R_1) of those digits
   uint32_t flags;        // bit 0: multiply outputs by ninv (single-pass inverse)
-  uint32_t ninv[N];      // n^-1 in Montgomery form
   size_t batch_stride;   // 32-bit words between batched transforms
 };
 
-template <int N, int MEMW>
-hipError_t launch_pass(int kind, int logr, const uint32_t* src, uint32_t* dst, const PassArgs<N>& A, uint32_t grid,
+template <class E>
+hipError_t launch_pass(int kind, int logr, const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t grid,
                        uint32_t batch, hipStream_t st);
-template <int N, int MEMW>
-hipError_t launch_naive(const uint32_t* src, uint32_t* dst, const PassArgs<N>& A, uint32_t batch, hipStream_t st);
-template <int N, int MEMW>
+template <class E>
+hipError_t launch_build_tw(uint32_t* out, size_t count, uint32_t log_s, uint32_t log_m, const uint32_t* lo,
+                           const uint32_t* hi, uint32_t lo_bits, const typename E::Args& F, hipStream_t st);
+template <class E>
+hipError_t launch_naive(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t batch, hipStream_t st);
+template <class E>
 hipError_t launch_fill(int kind, uint32_t* dst, size_t n, uint64_t seed, uint32_t nrand, uint32_t top_bits,
                        hipStream_t st);
-template <int N, int MEMW>
-hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, size_t n, const FieldArgs<N>& F,
-                            const Elem<N>& r2, hipStream_t st);
+// c = a * b (canonical in/out): mont(mont(a, b), R^2) with r2 in the engine table format
+template <class E>
+hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, size_t n, const typename E::Args& F,
+                            const uint32_t* d_r2, hipStream_t st);
 
 }  // namespace ntt

@@ -18,6 +18,7 @@
 #include <memory>
 #include <mutex>
 #include <tuple>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/ntt.h"
@@ -115,17 +116,96 @@ static void schedule(unsigned log_n, unsigned tile_log, unsigned* r, unsigned& p
   for (unsigned i = 0; i < p; ++i) r[i] = base + (i < rem ? 1 : 0);
 }
 
-template <int N, int MEMW>
+// ------------------------------------------------------------------------------ engine encodings
+// The host does all table arithmetic in 32-bit Montgomery form (HostField<NH>), produces canonical
+// values, then encodes them in the engine's own Montgomery domain / limb layout.
+template <class E>
+struct EngHost;
+
+template <int L, int W32>
+struct EngHost<Eng29<L, W32>> {
+  static constexpr int NH = W32;
+  using EA = typename Eng29<L, W32>::Args;
+  HostField<NH> const* H = nullptr;
+  Vec<NH> kR{};  // 2^(29L) mod p, canonical
+  void init(const HostField<NH>& h) {
+    H = &h;
+    Vec<NH> x{};
+    x[0] = 1;
+    for (int k = 0; k < 29 * L; ++k) x = h.add(x, x);
+    kR = x;
+  }
+  // canonical c -> c * 2^(29L) mod p as TW words
+  void encode(const Vec<NH>& c, uint32_t* out) const {
+    Vec<NH> m = H->mul(c, H->to_mont(kR));  // mont32(c, kR * R32) = c * kR
+    uint32_t w[NH], x[L];
+    for (int i = 0; i < NH; ++i) w[i] = m[i];
+    pack29<L, NH>(x, w);
+    for (int i = 0; i < Eng29<L, W32>::TW; ++i) out[i] = i < L ? x[i] : 0u;
+  }
+  bool check_modulus(const uint32_t* p) const {
+    // p < 2^(32*W32 - 1) so that 2p fits the HBM words and 16p < R = 2^(29L)
+    return (p[NH - 1] >> 31) == 0 && 29 * L >= 32 * NH - 1 + 4;
+  }
+  void fill_args(EA& A, const uint32_t* p, const Vec<NH>* w8, const Vec<NH>& ninv) const {
+    uint32_t pw[NH], p2w[NH];
+    uint32_t c = 0;
+    for (int i = 0; i < NH; ++i) {
+      pw[i] = p[i];
+      const uint64_t s = (uint64_t)p[i] + p[i] + c;
+      p2w[i] = (uint32_t)s;
+      c = (uint32_t)(s >> 32);
+    }
+    pack29<L, NH>(A.M.p, pw);
+    pack29<L, NH>(A.M.p2, p2w);
+    uint32_t inv = 1;
+    for (int i = 0; i < 5; ++i) inv *= 2 - p[0] * inv;
+    A.M.pinv = (0u - inv) & kMask29;
+    uint32_t tmp[Eng29<L, W32>::TW];
+    for (int k = 0; k < 3; ++k) {
+      encode(w8[k], tmp);
+      for (int i = 0; i < L; ++i) A.w8[k][i] = tmp[i];
+    }
+    encode(ninv, tmp);
+    for (int i = 0; i < L; ++i) A.ninv[i] = tmp[i];
+  }
+};
+
+template <int N, int MEMW_>
+struct EngHost<Eng32<N, MEMW_>> {
+  static constexpr int NH = N;
+  using EA = typename Eng32<N, MEMW_>::Args;
+  HostField<NH> const* H = nullptr;
+  void init(const HostField<NH>& h) { H = &h; }
+  void encode(const Vec<NH>& c, uint32_t* out) const {
+    const Vec<NH> m = H->to_mont(c);
+    for (int i = 0; i < N; ++i) out[i] = m[i];
+  }
+  bool check_modulus(const uint32_t* p) const { return p[NH - 1] < 0x7fffffffu; }
+  void fill_args(EA& A, const uint32_t* p, const Vec<NH>* w8, const Vec<NH>& ninv) const {
+    A.M = H->M;
+    for (int k = 0; k < 3; ++k) encode(w8[k], A.w8[k]);
+    encode(ninv, A.ninv);
+  }
+};
+
+template <class E>
 struct PlanImpl final : PlanBase {
-  HostField<N> H;
-  FieldArgs<N> Ff{}, Fi{};
-  Elem<N> ninv_m{}, r2_e{};
+  static constexpr int NH = EngHost<E>::NH;
+  static constexpr int TW = E::TW;
+  static constexpr int MEMW = E::MEMW;
+  HostField<NH> H;
+  EngHost<E> EH;
+  typename E::Args Ff{}, Fi{};
   uint32_t* d_tab = nullptr;
   uint32_t* d_scratch = nullptr;
+  uint32_t* d_full = nullptr;  // per-pass outer twiddle tables (HBM element format), both directions
+  size_t full_off[2][8] = {};  // element offsets into d_full, [dir][pass]
+  bool use_full = false;
   size_t scratch_elems = 0;
   // table word offsets
   size_t off_int_f[8] = {0}, off_int_i[8] = {0};
-  size_t off_lo_f = 0, off_hi_f = 0, off_lo_i = 0, off_hi_i = 0, off_hi_is = 0;
+  size_t off_lo_f = 0, off_hi_f = 0, off_lo_i = 0, off_hi_i = 0, off_hi_is = 0, off_r2 = 0;
   unsigned lo_bits = 0;
   uint32_t nrand = 1, top_bits = 28;
 
@@ -135,120 +215,121 @@ struct PlanImpl final : PlanBase {
     hipSetDevice(device);
     if (d_tab) hipFree(d_tab);
     if (d_scratch) hipFree(d_scratch);
+    if (d_full) hipFree(d_full);
     for (auto& row : ev)
       for (auto& e : row)
         if (e) hipEventDestroy(e);
     hipSetDevice(cur);
   }
 
-  // modulus / generator as N 32-bit words
+  // modulus / generator as NH 32-bit words
   int init(const uint32_t* p, const uint32_t* g, unsigned log_n_, int dev) {
     device = dev;
     log_n = log_n_;
     n = 1ull << log_n;
     elem_bytes = 4 * MEMW;
-    // ---- modulus checks: odd, top word < 2^31 - 1 (no-carry Montgomery), p > 2
-    for (int i = 0; i < N; ++i) H.M.p[i] = p[i];
+    // ---- modulus checks: odd, top word < 2^31 - 1 (no-carry host Montgomery)
+    for (int i = 0; i < NH; ++i) H.M.p[i] = p[i];
     if (!(p[0] & 1)) return NTT_ERR_FIELD;
-    if (p[N - 1] >= 0x7fffffffu) return NTT_ERR_FIELD;
+    if (p[NH - 1] >= 0x7fffffffu) return NTT_ERR_FIELD;
+    EH.init(H);
+    if (!EH.check_modulus(p)) return NTT_ERR_FIELD;
     uint32_t inv = 1;
     for (int i = 0; i < 5; ++i) inv *= 2 - p[0] * inv;
     H.M.pinv = 0u - inv;
-    // R mod p, R^2 mod p by doubling
-    Vec<N> x{};
-    x[0] = 1;
-    for (int k = 0; k < 32 * N; ++k) x = H.add(x, x);
-    H.r1 = x;
-    for (int k = 0; k < 32 * N; ++k) x = H.add(x, x);
-    H.r2 = x;
-    Vec<N> pv;
-    for (int i = 0; i < N; ++i) pv[i] = p[i];
-    Vec<N> gv;
-    for (int i = 0; i < N; ++i) gv[i] = g[i];
-    if (!vec_lt<N>(gv, pv)) return NTT_ERR_FIELD;
+    // R mod p, R^2 mod p by doubling (R = 2^(32 NH))
+    {
+      Vec<NH> x{};
+      x[0] = 1;
+      for (int k = 0; k < 32 * NH; ++k) x = H.add(x, x);
+      H.r1 = x;
+      for (int k = 0; k < 32 * NH; ++k) x = H.add(x, x);
+      H.r2 = x;
+    }
+    EH.init(H);  // needs r2 for to_mont
+    Vec<NH> pv, gv;
+    for (int i = 0; i < NH; ++i) {
+      pv[i] = p[i];
+      gv[i] = g[i];
+    }
+    if (!vec_lt<NH>(gv, pv)) return NTT_ERR_FIELD;
     // (p - 1) >> log_n, and n | p - 1
-    std::vector<uint32_t> pm1(p, p + N);
+    std::vector<uint32_t> pm1(p, p + NH);
     pm1[0] -= 1;  // p odd: no borrow
     for (unsigned b = 0; b < log_n; ++b)
       if ((pm1[b / 32] >> (b % 32)) & 1) return NTT_ERR_FIELD;
-    std::vector<uint32_t> e(N, 0);
-    for (int i = 0; i < N; ++i) {
+    std::vector<uint32_t> e(NH, 0);
+    for (int i = 0; i < NH; ++i) {
       const unsigned wsh = log_n / 32, bsh = log_n % 32;
-      uint64_t lo = (i + wsh < (unsigned)N) ? pm1[i + wsh] : 0;
-      uint64_t hi = (i + wsh + 1 < (unsigned)N) ? pm1[i + wsh + 1] : 0;
+      uint64_t lo = (i + wsh < (unsigned)NH) ? pm1[i + wsh] : 0;
+      uint64_t hi = (i + wsh + 1 < (unsigned)NH) ? pm1[i + wsh + 1] : 0;
       e[i] = (uint32_t)(((hi << 32) | lo) >> bsh);
     }
-    const Vec<N> gm = H.to_mont(gv);
-    const Vec<N> w = H.pow(gm, e);  // w_n (Montgomery)
-    // primitive: w^(n/2) == -1 (n >= 2)
-    if (log_n >= 1) {
-      Vec<N> pm1v;
-      for (int i = 0; i < N; ++i) pm1v[i] = pm1[i];
-      const Vec<N> h = H.from_mont(H.pow_u64(w, n / 2));
-      if (h != pm1v) return NTT_ERR_FIELD;
+    const Vec<NH> gm = H.to_mont(gv);
+    const Vec<NH> w = H.pow(gm, e);  // w_n (32-bit Montgomery form)
+    if (log_n >= 1) {                // primitive: w^(n/2) == -1
+      Vec<NH> pm1v;
+      for (int i = 0; i < NH; ++i) pm1v[i] = pm1[i];
+      if (H.from_mont(H.pow_u64(w, n / 2)) != pm1v) return NTT_ERR_FIELD;
     }
-    std::vector<uint32_t> pm2(p, p + N);  // p - 2 with borrow (BLS12-381 Fr has p[0] = 1)
+    std::vector<uint32_t> pm2(p, p + NH);  // p - 2 with borrow (BLS12-381 Fr has p[0] = 1)
     {
       uint64_t br = 2;
-      for (int i = 0; i < N && br; ++i) {
+      for (int i = 0; i < NH && br; ++i) {
         const uint64_t d = (uint64_t)pm2[i] - br;
         pm2[i] = (uint32_t)d;
         br = (d >> 63) & 1;
       }
     }
-    const Vec<N> winv = H.pow(w, pm2);
-    Vec<N> nv{};
+    const Vec<NH> winv = H.pow(w, pm2);
+    Vec<NH> nv{};
     nv[0] = (uint32_t)n;
-    if (N > 1) nv[1] = (uint32_t)(n >> 32);
-    const Vec<N> ninv = H.pow(H.to_mont(nv), pm2);
-    for (int i = 0; i < N; ++i) {
-      ninv_m.w[i] = ninv[i];
-      r2_e.w[i] = H.r2[i];
-    }
-    // field args per direction
-    auto fill_args = [&](FieldArgs<N>& F, const Vec<N>& wn) {
-      F.M = H.M;
-      Vec<N> w8 = (log_n >= 3) ? H.pow_u64(wn, n / 8) : H.r1;
-      Vec<N> acc = w8;
+    if (NH > 1) nv[1] = (uint32_t)(n >> 32);
+    const Vec<NH> ninv_c = H.from_mont(H.pow(H.to_mont(nv), pm2));
+    // field args per direction: w_8^k canonical
+    auto fill_args = [&](typename E::Args& F, const Vec<NH>& wn) {
+      const Vec<NH> w8m = (log_n >= 3) ? H.pow_u64(wn, n / 8) : H.r1;
+      Vec<NH> acc = w8m, w8c[3];
       for (int k = 0; k < 3; ++k) {
-        for (int i = 0; i < N; ++i) F.w8[k][i] = acc[i];
-        acc = H.mul(acc, w8);
+        w8c[k] = H.from_mont(acc);
+        acc = H.mul(acc, w8m);
       }
-      for (int i = 0; i < N; ++i) F.one[i] = H.r1[i];
+      EH.fill_args(F, p, w8c, ninv_c);
     };
     fill_args(Ff, w);
     fill_args(Fi, winv);
 
     // random-fill parameters: top nonzero 64-bit limb of p, masked to bitlen-1 bits
     {
-      const int L64 = (N + 1) / 2;
+      const int L64 = (NH + 1) / 2;
       int top = 0;
       for (int i = L64 - 1; i >= 0; --i) {
-        const uint64_t limb = (uint64_t)p[2 * i] | ((2 * i + 1 < N) ? (uint64_t)p[2 * i + 1] << 32 : 0);
+        const uint64_t limb = (uint64_t)p[2 * i] | ((2 * i + 1 < NH) ? (uint64_t)p[2 * i + 1] << 32 : 0);
         if (limb) { top = i; break; }
       }
-      const uint64_t tl = (uint64_t)p[2 * top] | ((2 * top + 1 < N) ? (uint64_t)p[2 * top + 1] << 32 : 0);
+      const uint64_t tl = (uint64_t)p[2 * top] | ((2 * top + 1 < NH) ? (uint64_t)p[2 * top + 1] << 32 : 0);
       nrand = top + 1;
       top_bits = 63 - __builtin_clzll(tl);  // bitlen - 1
     }
 
-    // ---- schedule + tables
-    schedule(log_n, tile_log(N), r, npass);
+    // ---- schedule + tables (engine-encoded)
+    schedule(log_n, tile_log_w(E::LDSW), r, npass);
     std::vector<uint32_t> host;
-    auto push_powers = [&](const Vec<N>& base, uint64_t count, const Vec<N>* scale) -> size_t {
+    auto push_powers = [&](const Vec<NH>& base_m, uint64_t count, const Vec<NH>* scale_m) -> size_t {
       const size_t off = host.size();
-      Vec<N> cur = scale ? *scale : H.r1;
-      for (uint64_t e2 = 0; e2 < count; ++e2) {
-        host.insert(host.end(), cur.begin(), cur.end());
-        cur = H.mul(cur, base);
+      Vec<NH> cur = scale_m ? *scale_m : H.r1;
+      uint32_t enc[TW];
+      for (uint64_t k = 0; k < count; ++k) {
+        EH.encode(H.from_mont(cur), enc);
+        host.insert(host.end(), enc, enc + TW);
+        cur = H.mul(cur, base_m);
       }
-      // pad to 16 B
       while (host.size() % 4) host.push_back(0);
       return off;
     };
-    const Vec<N> ninv_v = ninv;
+    const Vec<NH> ninv_m = H.to_mont(ninv_c);
     for (int dir = 0; dir < 2; ++dir) {
-      const Vec<N>& wn = dir ? winv : w;
+      const Vec<NH>& wn = dir ? winv : w;
       size_t* off_int = dir ? off_int_i : off_int_f;
       if (npass == 0) {
         off_int[0] = push_powers(wn, n, nullptr);
@@ -258,7 +339,7 @@ struct PlanImpl final : PlanBase {
       if (npass >= 2) {
         lo_bits = (log_n + 1) / 2;
         const size_t lo = push_powers(wn, 1ull << lo_bits, nullptr);
-        const Vec<N> step = H.pow_u64(wn, 1ull << lo_bits);
+        const Vec<NH> step = H.pow_u64(wn, 1ull << lo_bits);
         const size_t hi = push_powers(step, 1ull << (log_n - lo_bits), nullptr);
         if (dir == 0) {
           off_lo_f = lo;
@@ -266,9 +347,16 @@ struct PlanImpl final : PlanBase {
         } else {
           off_lo_i = lo;
           off_hi_i = hi;
-          off_hi_is = push_powers(step, 1ull << (log_n - lo_bits), &ninv_v);
+          off_hi_is = push_powers(step, 1ull << (log_n - lo_bits), &ninv_m);
         }
       }
+    }
+    {  // R_e^2 mod p for the pointwise product = encode(R_e mod p), R_e the engine's Montgomery radix
+      off_r2 = host.size();
+      uint32_t enc[TW];
+      EH.encode(engine_radix_mod_p(), enc);
+      host.insert(host.end(), enc, enc + TW);
+      while (host.size() % 4) host.push_back(0);
     }
     int cur = 0;
     hipGetDevice(&cur);
@@ -278,8 +366,50 @@ struct PlanImpl final : PlanBase {
         hipMemcpy(d_tab, host.data(), host.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
       rc = NTT_ERR_HIP;
     if (rc == NTT_OK && npass >= 2) rc = ensure_scratch(1);
+    if (rc == NTT_OK && npass >= 2) rc = build_full_tables();
     hipSetDevice(cur);
     return rc;
+  }
+
+  // Full per-pass outer-twiddle tables: pass i needs N_i entries (N_1 = n, N_2 = n / R_1, ...),
+  // streamed from HBM like the data in pass 1 and L2-resident afterwards.  They replace the
+  // two-level lookup's extra Montgomery product per element.  Skipped when a direction's tables
+  // would exceed kFullTableMaxBytes (the two-level tables are then used).
+  static constexpr size_t kFullTableMaxBytes = 2ull << 30;
+  int build_full_tables() {
+    size_t elems = 0;
+    unsigned blk = log_n;
+    for (unsigned i = 0; i + 1 < npass; ++i) {
+      full_off[0][i] = elems;
+      elems += 1ull << blk;
+      blk -= r[i];
+    }
+    if (elems * MEMW * 4 > kFullTableMaxBytes) return NTT_OK;
+    if (hipMalloc(&d_full, 2 * elems * MEMW * 4) != hipSuccess) return NTT_ERR_HIP;
+    for (int dir = 0; dir < 2; ++dir) {
+      blk = log_n;
+      for (unsigned i = 0; i + 1 < npass; ++i) {
+        full_off[dir][i] = dir * elems + full_off[0][i];
+        const uint32_t* lo = d_tab + (dir ? off_lo_i : off_lo_f);
+        const uint32_t* hi = d_tab + (dir ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
+        if (launch_build_tw<E>(d_full + full_off[dir][i] * MEMW, 1ull << blk, blk - r[i], log_n - blk, lo, hi,
+                               lo_bits, dir ? Fi : Ff, nullptr) != hipSuccess)
+          return NTT_ERR_HIP;
+        blk -= r[i];
+      }
+    }
+    if (hipDeviceSynchronize() != hipSuccess) return NTT_ERR_HIP;
+    use_full = true;
+    return NTT_OK;
+  }
+
+  // canonical value of the engine's Montgomery radix R_e mod p
+  Vec<NH> engine_radix_mod_p() const {
+    if constexpr (std::is_same<E, Eng32<E::W, E::MEMW>>::value) {
+      return H.r1;  // 2^(32N) mod p
+    } else {
+      return EH.kR;  // 2^(29L) mod p
+    }
   }
 
   int ensure_scratch(unsigned batch) {
@@ -293,13 +423,12 @@ struct PlanImpl final : PlanBase {
     return NTT_OK;
   }
 
-  PassArgs<N> base_args(bool inverse) const {
-    PassArgs<N> A;
+  PassArgs<E> base_args(bool inverse) const {
+    PassArgs<E> A;
     memset(&A, 0, sizeof(A));
     A.F = inverse ? Fi : Ff;
     A.log_n = log_n;
     A.lo_bits = lo_bits;
-    for (int i = 0; i < N; ++i) A.ninv[i] = ninv_m.w[i];
     A.batch_stride = (size_t)n * MEMW;
     return A;
   }
@@ -312,35 +441,36 @@ struct PlanImpl final : PlanBase {
     hipError_t e = hipSuccess;
     begin(st);
     if (npass == 0) {
-      PassArgs<N> A = base_args(inverse);
+      PassArgs<E> A = base_args(inverse);
       A.tw_int = d_tab + off_int[0];
       A.flags = inverse ? 1u : 0u;
-      e = launch_naive<N, MEMW>(data, data, A, batch, st);
+      e = launch_naive<E>(data, data, A, batch, st);
       mark(st);
     } else if (npass == 1) {
-      PassArgs<N> A = base_args(inverse);
+      PassArgs<E> A = base_args(inverse);
       A.tw_int = d_tab + off_int[0];
       A.flags = inverse ? 1u : 0u;
-      e = launch_pass<N, MEMW>(KIND_SINGLE, (int)r[0], data, data, A, 1, batch, st);
+      e = launch_pass<E>(KIND_SINGLE, (int)r[0], data, data, A, 1, batch, st);
       mark(st);
     } else {
       if (int rc = ensure_scratch(batch)) return rc;
-      const uint32_t grid = (uint32_t)(n >> tile_log(N));
+      const uint32_t grid = (uint32_t)(n >> tile_log_w(E::LDSW));
       unsigned blk = log_n;
       for (unsigned i = 0; i + 1 < npass && e == hipSuccess; ++i) {
-        PassArgs<N> A = base_args(inverse);
+        PassArgs<E> A = base_args(inverse);
         A.tw_int = d_tab + off_int[i];
         A.tw_lo = d_tab + (inverse ? off_lo_i : off_lo_f);
         A.tw_hi = d_tab + (inverse ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
+        A.tw_full = use_full ? d_full + full_off[inverse ? 1 : 0][i] * MEMW : nullptr;
         A.log_blk = blk;
         A.log_m = log_n - blk;
         const uint32_t* src = (i == 0) ? data : d_scratch;
-        e = launch_pass<N, MEMW>(KIND_COLUMN, (int)r[i], src, d_scratch, A, grid, batch, st);
+        e = launch_pass<E>(KIND_COLUMN, (int)r[i], src, d_scratch, A, grid, batch, st);
         mark(st);
         blk -= r[i];
       }
       if (e == hipSuccess) {
-        PassArgs<N> A = base_args(inverse);
+        PassArgs<E> A = base_args(inverse);
         A.tw_int = d_tab + off_int[npass - 1];
         A.r1 = r[0];
         A.nmid = npass - 2;
@@ -352,7 +482,7 @@ struct PlanImpl final : PlanBase {
           for (unsigned j = 1; j < idx; ++j) off += r[j];
           A.mid_off[m] = off;
         }
-        e = launch_pass<N, MEMW>(KIND_FINAL, (int)r[npass - 1], d_scratch, data, A, grid, batch, st);
+        e = launch_pass<E>(KIND_FINAL, (int)r[npass - 1], d_scratch, data, A, grid, batch, st);
         mark(st);
       }
     }
@@ -361,14 +491,14 @@ struct PlanImpl final : PlanBase {
 
   int pointwise(const void* a, const void* b, void* c, hipStream_t st) override {
     if (!a || !b || !c) return NTT_ERR_ARG;
-    hipError_t e = launch_pointwise<N, MEMW>(static_cast<const uint32_t*>(a), static_cast<const uint32_t*>(b),
-                                             static_cast<uint32_t*>(c), n, Ff, r2_e, st);
+    hipError_t e = launch_pointwise<E>(static_cast<const uint32_t*>(a), static_cast<const uint32_t*>(b),
+                                       static_cast<uint32_t*>(c), n, Ff, d_tab + off_r2, st);
     return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
   }
 
   int fill(void* d, int kind, uint64_t seed, hipStream_t st) override {
     if (!d || (kind != 0 && kind != 1)) return NTT_ERR_ARG;
-    hipError_t e = launch_fill<N, MEMW>(kind, static_cast<uint32_t*>(d), n, seed, nrand, top_bits, st);
+    hipError_t e = launch_fill<E>(kind, static_cast<uint32_t*>(d), n, seed, nrand, top_bits, st);
     return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
   }
 };
@@ -400,15 +530,15 @@ static int make_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, const 
   int rc;
   if (limbs64 == 1) {
     if (p64[0] >= (1ull << 31)) return NTT_ERR_FIELD;  // `long long` path: 31-bit primes
-    auto impl = std::make_unique<PlanImpl<1, 2>>();
+    auto impl = std::make_unique<PlanImpl<EngP>>();
     rc = impl->init(p32, g32, log_n, device);
     out = std::move(impl);
   } else if (limbs64 == 4) {
-    auto impl = std::make_unique<PlanImpl<8, 8>>();
+    auto impl = std::make_unique<PlanImpl<Eng256>>();
     rc = impl->init(p32, g32, log_n, device);
     out = std::move(impl);
   } else if (limbs64 == 6) {
-    auto impl = std::make_unique<PlanImpl<12, 12>>();
+    auto impl = std::make_unique<PlanImpl<Eng384>>();
     rc = impl->init(p32, g32, log_n, device);
     out = std::move(impl);
   } else {
