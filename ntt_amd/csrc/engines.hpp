@@ -21,6 +21,7 @@ struct Eng29 {
   static constexpr int LDSW = L;            // words per element in LDS
   struct Args {
     Mod29<L> M;
+    uint32_t p4[L], p8[L];  // 4p, 8p (normalised) for the lazy butterflies
     uint32_t w8[3][L];  // w_8^1, w_8^2, w_8^3 (Montgomery, R = 2^(29L))
     uint32_t ninv[L];   // n^-1 (Montgomery)
   };
@@ -62,6 +63,47 @@ struct Eng29 {
 #pragma unroll
     for (int i = 0; i < W; ++i) x[i] = r[i];
   }
+  // ---- lazy DIF butterflies for the in-register DFTs: stage s (1-based) takes inputs < 2^s p and
+  // produces (a + b, a - b + K p) with K = 2^s, i.e. outputs < 2^(s+1) p.  Sums and differences are
+  // only carry-normalised (no conditional subtraction); values stay far below R = 2^(29L) (16p <
+  // 2^259), so every Montgomery product still returns < 2p.  reduce_to_2p() brings the outputs that
+  // are not multiplied afterwards back under 2p.
+  template <int K>
+  __device__ static __forceinline__ const uint32_t (&kp(const Args& A))[L] {
+    static_assert(K == 2 || K == 4 || K == 8, "lazy bound");
+    if constexpr (K == 2) return A.M.p2;
+    else if constexpr (K == 4) return A.p4;
+    else return A.p8;
+  }
+  template <int K>
+  __device__ static __forceinline__ void bfly_l(uint32_t (&a)[W], uint32_t (&b)[W], const Args& A) {
+    const uint32_t(&q)[L] = kp<K>(A);
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      const uint32_t x = a[i], y = b[i];
+      a[i] = x + y;
+      b[i] = x - y + q[i];
+    }
+    norm_u<L>(a);
+    norm_s<L>(b);
+  }
+  template <int K>
+  __device__ static __forceinline__ void bfly_w_l(uint32_t (&a)[W], uint32_t (&b)[W], const uint32_t (&w)[W],
+                                                  const Args& A) {
+    bfly_l<K>(a, b, A);
+    uint32_t r[W];
+    mont29<L>(r, b, w, A.M);
+#pragma unroll
+    for (int i = 0; i < W; ++i) b[i] = r[i];
+  }
+  // x < B p -> x < 2p (B a power of two <= 16)
+  template <int B>
+  __device__ static __forceinline__ void reduce_to_2p(uint32_t (&x)[W], const Args& A) {
+    if constexpr (B > 8) cond_sub<L>(x, A.p8);
+    if constexpr (B > 4) cond_sub<L>(x, A.p4);
+    if constexpr (B > 2) cond_sub<L>(x, A.M.p2);
+  }
+
   // DIF butterflies on lazy residues (< 2p in, < 2p out)
   __device__ static __forceinline__ void bfly(uint32_t (&a)[W], uint32_t (&b)[W], const Args& A) {
     uint32_t u[W], d[W];
@@ -124,6 +166,17 @@ struct Eng32 {
   __device__ static __forceinline__ void mul(uint32_t (&x)[W], const uint32_t (&w)[W], const Args& A) {
     mont_mul<N>(x, x, w, A.M);
   }
+  template <int K>
+  __device__ static __forceinline__ void bfly_l(uint32_t (&a)[W], uint32_t (&b)[W], const Args& A) {
+    bfly(a, b, A);
+  }
+  template <int K>
+  __device__ static __forceinline__ void bfly_w_l(uint32_t (&a)[W], uint32_t (&b)[W], const uint32_t (&w)[W],
+                                                  const Args& A) {
+    bfly_w(a, b, w, A);
+  }
+  template <int B>
+  __device__ static __forceinline__ void reduce_to_2p(uint32_t (&)[W], const Args&) {}
   __device__ static __forceinline__ void bfly(uint32_t (&a)[W], uint32_t (&b)[W], const Args& A) {
     uint32_t s[W], d[W];
     add_mod<N>(s, a, b, A.M);

@@ -62,30 +62,30 @@ __device__ __forceinline__ uint32_t natural_index(uint32_t pi) {
 }
 
 // In-register DFT of size Q in {2,4,8} over x[base + d], d < Q (DIF radix-2 network): output X_k
-// lands in slot base + brev(k).
+// lands in slot base + brev(k).  Lazy bounds (engines.hpp): inputs < 2p, outputs < 2Q p.
 template <class E, int Q, int base>
 __device__ __forceinline__ void dft_q(uint32_t (&x)[8][E::W], const typename E::Args& F) {
   if constexpr (Q == 2) {
-    E::bfly(x[base], x[base + 1], F);
+    E::template bfly_l<2>(x[base], x[base + 1], F);
   } else if constexpr (Q == 4) {
-    E::bfly(x[base], x[base + 2], F);
-    E::bfly_w(x[base + 1], x[base + 3], F.w8[1], F);
-    E::bfly(x[base], x[base + 1], F);
-    E::bfly(x[base + 2], x[base + 3], F);
+    E::template bfly_l<2>(x[base], x[base + 2], F);
+    E::template bfly_w_l<2>(x[base + 1], x[base + 3], F.w8[1], F);
+    E::template bfly_l<4>(x[base], x[base + 1], F);
+    E::template bfly_l<4>(x[base + 2], x[base + 3], F);
   } else {
     static_assert(Q == 8, "radix");
-    E::bfly(x[base], x[base + 4], F);
-    E::bfly_w(x[base + 1], x[base + 5], F.w8[0], F);
-    E::bfly_w(x[base + 2], x[base + 6], F.w8[1], F);
-    E::bfly_w(x[base + 3], x[base + 7], F.w8[2], F);
-    E::bfly(x[base], x[base + 2], F);
-    E::bfly_w(x[base + 1], x[base + 3], F.w8[1], F);
-    E::bfly(x[base + 4], x[base + 6], F);
-    E::bfly_w(x[base + 5], x[base + 7], F.w8[1], F);
-    E::bfly(x[base], x[base + 1], F);
-    E::bfly(x[base + 2], x[base + 3], F);
-    E::bfly(x[base + 4], x[base + 5], F);
-    E::bfly(x[base + 6], x[base + 7], F);
+    E::template bfly_l<2>(x[base], x[base + 4], F);
+    E::template bfly_w_l<2>(x[base + 1], x[base + 5], F.w8[0], F);
+    E::template bfly_w_l<2>(x[base + 2], x[base + 6], F.w8[1], F);
+    E::template bfly_w_l<2>(x[base + 3], x[base + 7], F.w8[2], F);
+    E::template bfly_l<4>(x[base], x[base + 2], F);
+    E::template bfly_w_l<4>(x[base + 1], x[base + 3], F.w8[1], F);
+    E::template bfly_l<4>(x[base + 4], x[base + 6], F);
+    E::template bfly_w_l<4>(x[base + 5], x[base + 7], F.w8[1], F);
+    E::template bfly_l<8>(x[base], x[base + 1], F);
+    E::template bfly_l<8>(x[base + 2], x[base + 3], F);
+    E::template bfly_l<8>(x[base + 4], x[base + 5], F);
+    E::template bfly_l<8>(x[base + 6], x[base + 7], F);
   }
 }
 
@@ -95,6 +95,14 @@ __device__ __forceinline__ void twiddle_mul(uint32_t (&x)[E::W], const uint32_t*
   uint32_t w[E::W];
   E::tload(w, tab, e);
   E::mul(x, w, F);
+}
+
+// LDS slot of (local column/block c, in-column position pi): column-minor like HBM, with c XOR-ed
+// by the low bits of pi so that both lane orders used (c fastest, or pi fastest) hit distinct
+// 16-byte slots (the final pass writes with pi fastest: 8-way conflicts without the swizzle).
+template <int T>
+__device__ __forceinline__ uint32_t lds_slot(uint32_t c, uint32_t pi) {
+  return (c ^ (pi & (T - 1))) + T * pi;
 }
 
 // One LDS exchange + in-register radix-Q sub-stage s (s >= 1).
@@ -111,7 +119,7 @@ __device__ __forceinline__ void substage(uint32_t (&x)[8][E::W], uint32_t (&cl)[
     static_for<PQ>([&](auto K) {
       constexpr int k = K;
       const uint32_t pi = (rho << plN) + cp + (k << psb);
-      lds_put<E::LDSW, TE>(lds, cl[j] + T * pi, x[j * PQ + brev_bits(k, pqb)]);
+      lds_put<E::LDSW, TE>(lds, lds_slot<T>(cl[j], pi), x[j * PQ + brev_bits(k, pqb)]);
     });
   });
   __syncthreads();
@@ -126,13 +134,14 @@ __device__ __forceinline__ void substage(uint32_t (&x)[8][E::W], uint32_t (&cl)[
     static_for<Q>([&](auto D) {
       constexpr int d = D;
       const uint32_t pi = (rho << lN) + cp + (d << sb);
-      lds_get<E::LDSW, TE>(x[j * Q + d], lds, c + T * pi);
+      lds_get<E::LDSW, TE>(x[j * Q + d], lds, lds_slot<T>(c, pi));
     });
   });
   static_for<G>([&](auto J) {
     constexpr int j = J;
     dft_q<E, Q, j * Q>(x, A.F);
     if constexpr (s + 1 < S::nsub) {
+      E::template reduce_to_2p<2 * Q>(x[j * Q], A.F);  // k = 0: the only output not multiplied
       const uint32_t cp = pil[j] & ((1u << sb) - 1);
       static_for<Q - 1>([&](auto K1) {
         constexpr int k = K1 + 1;
@@ -221,6 +230,7 @@ __global__ __launch_bounds__(256) void k_pass(const uint32_t* __restrict__ src, 
       constexpr int j = J;
       dft_q<E, Q, j * Q>(x, A.F);
       if constexpr (S::nsub > 1) {
+        E::template reduce_to_2p<2 * Q>(x[j * Q], A.F);  // k = 0: the only output not multiplied
         static_for<Q - 1>([&](auto K1) {
           constexpr int k = K1 + 1;
           twiddle_mul<E>(x[j * Q + brev_bits(k, qb)], A.tw_int, pil[j] * k, A.F);
@@ -266,9 +276,13 @@ __global__ __launch_bounds__(256) void k_pass(const uint32_t* __restrict__ src, 
           E::mul(v, tl, A.F);
           pos = colbase + c + ((size_t)kn << log_s);
         } else if constexpr (KIND == KIND_FINAL) {
+          E::template reduce_to_2p<2 * Q>(v, A.F);
           pos = (size_t)(k10 + c) + ((size_t)midrev << A.r1) + ((size_t)kn << (A.log_n - LOGR));
         } else {
-          if (A.flags & 1u) E::mul(v, A.F.ninv, A.F);
+          if (A.flags & 1u)
+            E::mul(v, A.F.ninv, A.F);
+          else
+            E::template reduce_to_2p<2 * Q>(v, A.F);
           pos = kn;
         }
         E::store(dst, pos, v, A.F);
@@ -393,19 +407,26 @@ __global__ void k_pointwise_mul(const uint32_t* __restrict__ a, const uint32_t* 
 }
 
 // ---------------------------------------------------------------------------- launchers
+// Radices the planner can emit: column/final passes use 3 <= r <= tile_log - 2, single-workgroup
+// transforms 3 <= r <= tile_log.  Only those are instantiated.
 template <class E, int KIND, int LOGR>
 static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t grid,
                                 uint32_t batch, hipStream_t st) {
-  constexpr int TE = (KIND == KIND_SINGLE) ? (1 << LOGR) : tile_elems_w(E::LDSW);
-  if constexpr ((1 << LOGR) > TE) {
+  constexpr int TL = tile_log_w(E::LDSW);
+  constexpr int MAXR = (KIND == KIND_SINGLE) ? TL : TL - 2;
+  if constexpr (LOGR > MAXR) {
     return hipErrorInvalidValue;
   } else {
+    constexpr int TE = (KIND == KIND_SINGLE) ? (1 << LOGR) : (1 << TL);
     constexpr int NT = TE / 8;
     const dim3 g(grid, batch), b(NT < 64 ? 64 : NT);
-    if (KIND == KIND_COLUMN && A.tw_full)
-      hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true>), g, b, 0, st, src, dst, A);
-    else
-      hipLaunchKernelGGL((k_pass<E, LOGR, KIND, false>), g, b, 0, st, src, dst, A);
+    if constexpr (KIND == KIND_COLUMN) {
+      if (A.tw_full) {
+        hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true>), g, b, 0, st, src, dst, A);
+        return hipGetLastError();
+      }
+    }
+    hipLaunchKernelGGL((k_pass<E, LOGR, KIND, false>), g, b, 0, st, src, dst, A);
     return hipGetLastError();
   }
 }

@@ -158,6 +158,13 @@ struct EngHost<Eng29<L, W32>> {
     }
     pack29<L, NH>(A.M.p, pw);
     pack29<L, NH>(A.M.p2, p2w);
+    // 4p, 8p: shift the normalised 2p limbs left and renormalise (values < 2^(29L))
+    for (int i = 0; i < L; ++i) {
+      A.p4[i] = A.M.p2[i] << 1;
+      A.p8[i] = A.M.p2[i] << 2;
+    }
+    norm_u<L>(A.p4);
+    norm_u<L>(A.p8);
     uint32_t inv = 1;
     for (int i = 0; i < 5; ++i) inv *= 2 - p[0] * inv;
     A.M.pinv = (0u - inv) & kMask29;
