@@ -55,10 +55,17 @@ typedef struct ntt_plan ntt_plan;
  * (big-num.cu:278-309). */
 int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device);
 
+/* Plan flags for the _ex constructors. */
+#define NTT_PLAN_TWIDDLE_ONLY 1u /* only the w_n tables: fill / twiddle_pack / transpose, no transforms */
+int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags);
+
 /* Modulus-generic plan, like big-num.cu's `prime` / `omega` kernel arguments (big-num.cu:68,173,260):
  * modulus and generator given as limbs64 little-endian 64-bit limbs. */
 int ntt_plan_create_custom(ntt_plan** out, const uint64_t* modulus, const uint64_t* generator, unsigned limbs64,
                            unsigned log_n, int device);
+
+int ntt_plan_create_custom_ex(ntt_plan** out, const uint64_t* modulus, const uint64_t* generator, unsigned limbs64,
+                              unsigned log_n, int device, unsigned flags);
 
 /* Forward NTT in place, natural -> natural (SSIP GZKP-NTT.cu:1452, NTT_GZKP big-num.cu:260). */
 int ntt_forward(ntt_plan* plan, void* d_data, void* hip_stream);
@@ -77,6 +84,23 @@ int ntt_polymul(ntt_plan* plan, void* d_a, void* d_b, void* d_c, void* hip_strea
 /* Fill a device vector with the SURVEY §8d synthetic inputs: kind 0 = x_j = j (the reference's
  * input, GZKP-NTT.cu:1587), kind 1 = SplitMix64 limbs with the top limb masked (seeded). */
 int ntt_fill(ntt_plan* plan, void* d_data, int kind, uint64_t seed, void* hip_stream);
+
+/* Fill `count` local elements: element i gets the synthetic value of global index
+ * j = row0 + (i >> log_inner) + ((i mod 2^log_inner) << log_stride)  (log_inner >= 64: j = i).
+ * Used to lay out one rank's share of a distributed vector. */
+int ntt_fill_map(ntt_plan* plan, void* d_data, uint64_t count, int kind, uint64_t seed, uint64_t row0,
+                 unsigned log_inner, unsigned log_stride, void* hip_stream);
+
+/* ---------------------------------------------------------------- multi-GPU four-step, local steps
+ * (the exchange itself is an RCCL all-to-all issued by the caller)
+ * twiddle_pack: src = [2^log_rows][2^log_row_len] row-major; element (a, b) is multiplied by
+ * w_n^((row0 + a) * b) (w_n^-1 if inverse; n = 2^log_n of the plan) and written to
+ * dst[b >> log_block][a][b mod 2^log_block]: one contiguous chunk per destination rank.
+ * transpose: dst[c][r] = src[r][c] for a 2^log_rows x 2^log_cols matrix of elements. */
+int ntt_twiddle_pack(ntt_plan* plan, const void* d_src, void* d_dst, unsigned log_rows, unsigned log_row_len,
+                     unsigned log_block, uint64_t row0, int inverse, void* hip_stream);
+int ntt_transpose(ntt_plan* plan, const void* d_src, void* d_dst, unsigned log_rows, unsigned log_cols,
+                  void* hip_stream);
 
 /* Per-launch timing for benchmarks: when enabled, every transform records HIP events on its
  * stream between its kernel launches (a ring of 64 transforms, no host synchronisation);

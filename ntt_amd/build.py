@@ -18,7 +18,7 @@ BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libntt.so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
-SOURCES = ["ntt_k8.hip", "ntt_k12.hip", "ntt_k1.hip", "ntt_plan.cpp", "ntt_dist.cpp"]
+SOURCES = ["ntt_k8.hip", "ntt_k12.hip", "ntt_k1.hip", "ntt_plan.cpp"]
 ARCH = os.environ.get("NTT_OFFLOAD_ARCH", "gfx950")
 
 

@@ -44,9 +44,17 @@ hipError_t launch_build_tw(uint32_t* out, size_t count, uint32_t log_s, uint32_t
                            const uint32_t* hi, uint32_t lo_bits, const typename E::Args& F, hipStream_t st);
 template <class E>
 hipError_t launch_naive(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t batch, hipStream_t st);
+// Fill local element i with the synthetic value of global index
+// j = row0 + (i >> log_inner) + ((i mod 2^log_inner) << log_stride)   (log_inner = 64: j = i).
 template <class E>
 hipError_t launch_fill(int kind, uint32_t* dst, size_t n, uint64_t seed, uint32_t nrand, uint32_t top_bits,
-                       hipStream_t st);
+                       uint64_t row0, uint32_t log_inner, uint32_t log_stride, hipStream_t st);
+template <class E>
+hipError_t launch_twiddle_pack(const uint32_t* src, uint32_t* dst, uint32_t log_rows, uint32_t log_len,
+                               uint32_t log_bw, uint64_t row0, uint32_t log_n, const uint32_t* lo, const uint32_t* hi,
+                               uint32_t lo_bits, const typename E::Args& F, hipStream_t st);
+template <class E>
+hipError_t launch_transpose(const uint32_t* src, uint32_t* dst, uint32_t log_rows, uint32_t log_cols, hipStream_t st);
 // c = a * b (canonical in/out): mont(mont(a, b), R^2) with r2 in the engine table format
 template <class E>
 hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, size_t n, const typename E::Args& F,

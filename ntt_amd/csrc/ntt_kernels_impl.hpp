@@ -343,6 +343,76 @@ hipError_t launch_build_tw(uint32_t* out, size_t count, uint32_t log_s, uint32_t
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------- four-step helpers
+// Multi-GPU four-step, local steps.  twiddle_pack: src is [rows][row_len] (row-major);
+// element (a, b) is multiplied by w_n^((row0 + a) * b) and written to dst block b / bw (bw =
+// row_len / G) at a * bw + b % bw, i.e. dst = [G][rows][bw]: one contiguous chunk per peer for the
+// all-to-all.  Twiddles from the plan's two-level tables (w_n^e = lo[e & mask] * hi[e >> lo_bits]).
+template <class E>
+__global__ void k_twiddle_pack(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t log_rows,
+                               uint32_t log_len, uint32_t log_bw, uint64_t row0, uint32_t log_n,
+                               const uint32_t* __restrict__ lo, const uint32_t* __restrict__ hi, uint32_t lo_bits,
+                               const typename E::Args F) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (1ull << (log_rows + log_len))) return;
+  const uint64_t a = i >> log_len, b = i & ((1ull << log_len) - 1);
+  const uint64_t e = ((row0 + a) * b) & ((1ull << log_n) - 1);
+  uint32_t x[E::W], w[E::W], h[E::W];
+  E::load(x, src, i);
+  E::tload(w, lo, (uint32_t)(e & ((1ull << lo_bits) - 1)));
+  E::tload(h, hi, (uint32_t)(e >> lo_bits));
+  E::mul(w, h, F);
+  E::mul(x, w, F);
+  const size_t blk = b >> log_bw, off = b & ((1ull << log_bw) - 1);
+  E::store(dst, (blk << (log_rows + log_bw)) + (a << log_bw) + off, x, F);
+}
+
+// dst[c][r] = src[r][c] for a rows x cols matrix of MEMW-word elements (32x32 tiles through LDS).
+template <int MEMW>
+__global__ void k_transpose(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t log_rows,
+                            uint32_t log_cols) {
+  constexpr int TILE = 32;
+  __shared__ uint32_t tile[TILE][TILE + 1][MEMW];
+  const uint64_t rows = 1ull << log_rows, cols = 1ull << log_cols;
+  const uint64_t bx = (uint64_t)blockIdx.x * TILE, by = (uint64_t)blockIdx.y * TILE;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 32 x 8
+  for (int k = ty; k < TILE; k += 8) {
+    const uint64_t r = by + k, c = bx + tx;
+    if (r < rows && c < cols) {
+      const uint32_t* s = src + (r * cols + c) * MEMW;
+#pragma unroll
+      for (int w = 0; w < MEMW; ++w) tile[k][tx][w] = s[w];
+    }
+  }
+  __syncthreads();
+  for (int k = ty; k < TILE; k += 8) {
+    const uint64_t c = bx + k, r = by + tx;
+    if (r < rows && c < cols) {
+      uint32_t* d = dst + (c * rows + r) * MEMW;
+#pragma unroll
+      for (int w = 0; w < MEMW; ++w) d[w] = tile[tx][k][w];
+    }
+  }
+}
+
+template <class E>
+hipError_t launch_twiddle_pack(const uint32_t* src, uint32_t* dst, uint32_t log_rows, uint32_t log_len,
+                               uint32_t log_bw, uint64_t row0, uint32_t log_n, const uint32_t* lo, const uint32_t* hi,
+                               uint32_t lo_bits, const typename E::Args& F, hipStream_t st) {
+  const size_t total = 1ull << (log_rows + log_len);
+  hipLaunchKernelGGL((k_twiddle_pack<E>), dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, st, src, dst, log_rows,
+                     log_len, log_bw, row0, log_n, lo, hi, lo_bits, F);
+  return hipGetLastError();
+}
+
+template <class E>
+hipError_t launch_transpose(const uint32_t* src, uint32_t* dst, uint32_t log_rows, uint32_t log_cols, hipStream_t st) {
+  const uint64_t rows = 1ull << log_rows, cols = 1ull << log_cols;
+  const dim3 grid((uint32_t)((cols + 31) / 32), (uint32_t)((rows + 31) / 32));
+  hipLaunchKernelGGL((k_transpose<E::MEMW>), grid, dim3(256), 0, st, src, dst, log_rows, log_cols);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------- utility kernels
 __device__ __forceinline__ uint64_t splitmix64(uint64_t c) {
   uint64_t z = c + 0x9E3779B97F4A7C15ull;
@@ -353,13 +423,25 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t c) {
 
 // SURVEY §8d vector B: limb_i = SplitMix64(seed*2^32 + 4j + i) (64-bit limbs), limbs at and above
 // `nrand` zero, the top random limb masked to `top_bits` so that every value is < p.
+struct FillMap {
+  uint64_t row0;       // global index of local row 0
+  uint32_t log_inner;  // local row length (log2); 64 = identity map
+  uint32_t log_stride; // global stride of the inner index (log2)
+};
+__device__ __forceinline__ uint64_t fill_index(size_t i, const FillMap& m) {
+  if (m.log_inner >= 64) return i;
+  return m.row0 + (i >> m.log_inner) + ((uint64_t)(i & ((1ull << m.log_inner) - 1)) << m.log_stride);
+}
+
 template <int MEMW>
-__global__ void k_fill_random(uint32_t* __restrict__ dst, size_t n, uint64_t seed, uint32_t nrand, uint32_t top_bits) {
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
+__global__ void k_fill_random(uint32_t* __restrict__ dst, size_t n, uint64_t seed, uint32_t nrand, uint32_t top_bits,
+                              FillMap fm) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t j = fill_index(i, fm);
   if constexpr (MEMW == 2) {
     const uint64_t v = splitmix64((seed << 32) + 4 * j) & ((1ull << top_bits) - 1);
-    reinterpret_cast<uint2*>(dst)[j] = make_uint2((uint32_t)v, 0u);
+    reinterpret_cast<uint2*>(dst)[i] = make_uint2((uint32_t)v, 0u);
   } else {
     uint32_t v[MEMW];
 #pragma unroll
@@ -372,20 +454,21 @@ __global__ void k_fill_random(uint32_t* __restrict__ dst, size_t n, uint64_t see
       v[2 * i] = (uint32_t)limb;
       v[2 * i + 1] = (uint32_t)(limb >> 32);
     }
-    uint4* p = reinterpret_cast<uint4*>(dst + j * MEMW);
+    uint4* p = reinterpret_cast<uint4*>(dst + i * MEMW);
 #pragma unroll
     for (int q = 0; q < MEMW / 4; ++q) p[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
   }
 }
 
 template <int MEMW>
-__global__ void k_fill_iota(uint32_t* __restrict__ dst, size_t n) {
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
+__global__ void k_fill_iota(uint32_t* __restrict__ dst, size_t n, FillMap fm) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t j = fill_index(i, fm);
   if constexpr (MEMW == 2) {
-    reinterpret_cast<uint2*>(dst)[j] = make_uint2((uint32_t)j, (uint32_t)((uint64_t)j >> 32));
+    reinterpret_cast<uint2*>(dst)[i] = make_uint2((uint32_t)j, (uint32_t)((uint64_t)j >> 32));
   } else {
-    uint4* p = reinterpret_cast<uint4*>(dst + j * MEMW);
+    uint4* p = reinterpret_cast<uint4*>(dst + i * MEMW);
     p[0] = make_uint4((uint32_t)j, (uint32_t)((uint64_t)j >> 32), 0u, 0u);
 #pragma unroll
     for (int q = 1; q < MEMW / 4; ++q) p[q] = make_uint4(0u, 0u, 0u, 0u);
@@ -464,12 +547,13 @@ hipError_t launch_naive(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A
 
 template <class E>
 hipError_t launch_fill(int kind, uint32_t* dst, size_t n, uint64_t seed, uint32_t nrand, uint32_t top_bits,
-                       hipStream_t st) {
+                       uint64_t row0, uint32_t log_inner, uint32_t log_stride, hipStream_t st) {
   const uint32_t blocks = (uint32_t)((n + 255) / 256);
+  const FillMap fm{row0, log_inner, log_stride};
   if (kind == 0)
-    hipLaunchKernelGGL((k_fill_iota<E::MEMW>), dim3(blocks), dim3(256), 0, st, dst, n);
+    hipLaunchKernelGGL((k_fill_iota<E::MEMW>), dim3(blocks), dim3(256), 0, st, dst, n, fm);
   else
-    hipLaunchKernelGGL((k_fill_random<E::MEMW>), dim3(blocks), dim3(256), 0, st, dst, n, seed, nrand, top_bits);
+    hipLaunchKernelGGL((k_fill_random<E::MEMW>), dim3(blocks), dim3(256), 0, st, dst, n, seed, nrand, top_bits, fm);
   return hipGetLastError();
 }
 
@@ -485,7 +569,12 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
   template hipError_t launch_pass<E>(int, int, const uint32_t*, uint32_t*, const PassArgs<E>&, uint32_t, uint32_t, \
                                      hipStream_t);                                                                 \
   template hipError_t launch_naive<E>(const uint32_t*, uint32_t*, const PassArgs<E>&, uint32_t, hipStream_t);       \
-  template hipError_t launch_fill<E>(int, uint32_t*, size_t, uint64_t, uint32_t, uint32_t, hipStream_t);           \
+  template hipError_t launch_fill<E>(int, uint32_t*, size_t, uint64_t, uint32_t, uint32_t, uint64_t, uint32_t,     \
+                                     uint32_t, hipStream_t);                                                       \
+  template hipError_t launch_twiddle_pack<E>(const uint32_t*, uint32_t*, uint32_t, uint32_t, uint32_t, uint64_t,   \
+                                             uint32_t, const uint32_t*, const uint32_t*, uint32_t,                 \
+                                             const typename E::Args&, hipStream_t);                                \
+  template hipError_t launch_transpose<E>(const uint32_t*, uint32_t*, uint32_t, uint32_t, hipStream_t);           \
   template hipError_t launch_pointwise<E>(const uint32_t*, const uint32_t*, uint32_t*, size_t,                     \
                                           const typename E::Args&, const uint32_t*, hipStream_t);                  \
   template hipError_t launch_build_tw<E>(uint32_t*, size_t, uint32_t, uint32_t, const uint32_t*, const uint32_t*,  \

@@ -81,8 +81,13 @@ struct PlanBase {
   virtual ~PlanBase() = default;
   virtual int run(void* d, unsigned batch, bool inverse, hipStream_t st) = 0;
   virtual int pointwise(const void* a, const void* b, void* c, hipStream_t st) = 0;
-  virtual int fill(void* d, int kind, uint64_t seed, hipStream_t st) = 0;
+  virtual int fill(void* d, uint64_t count, int kind, uint64_t seed, uint64_t row0, unsigned log_inner,
+                   unsigned log_stride, hipStream_t st) = 0;
+  virtual int twiddle_pack(const void* src, void* dst, unsigned log_rows, unsigned log_len, unsigned log_bw,
+                           uint64_t row0, bool inverse, hipStream_t st) = 0;
+  virtual int transpose(const void* src, void* dst, unsigned log_rows, unsigned log_cols, hipStream_t st) = 0;
   uint64_t n = 0;
+  unsigned flags = 0;
   unsigned log_n = 0, elem_bytes = 0, npass = 0;
   unsigned r[8] = {0};
   int device = 0;
@@ -230,8 +235,9 @@ struct PlanImpl final : PlanBase {
   }
 
   // modulus / generator as NH 32-bit words
-  int init(const uint32_t* p, const uint32_t* g, unsigned log_n_, int dev) {
+  int init(const uint32_t* p, const uint32_t* g, unsigned log_n_, int dev, unsigned flags_) {
     device = dev;
+    flags = flags_;
     log_n = log_n_;
     n = 1ull << log_n;
     elem_bytes = 4 * MEMW;
@@ -321,6 +327,7 @@ struct PlanImpl final : PlanBase {
 
     // ---- schedule + tables (engine-encoded)
     schedule(log_n, tile_log_w(E::LDSW), r, npass);
+    const bool twiddle_only = (flags & NTT_PLAN_TWIDDLE_ONLY) != 0;
     std::vector<uint32_t> host;
     auto push_powers = [&](const Vec<NH>& base_m, uint64_t count, const Vec<NH>* scale_m) -> size_t {
       const size_t off = host.size();
@@ -338,12 +345,14 @@ struct PlanImpl final : PlanBase {
     for (int dir = 0; dir < 2; ++dir) {
       const Vec<NH>& wn = dir ? winv : w;
       size_t* off_int = dir ? off_int_i : off_int_f;
-      if (npass == 0) {
+      if (twiddle_only) {
+        // no transform tables
+      } else if (npass == 0) {
         off_int[0] = push_powers(wn, n, nullptr);
       } else {
         for (unsigned i = 0; i < npass; ++i) off_int[i] = push_powers(H.pow_u64(wn, n >> r[i]), 1ull << r[i], nullptr);
       }
-      if (npass >= 2) {
+      {  // two-level tables of w_n^e (outer twiddles, four-step twiddle_pack)
         lo_bits = (log_n + 1) / 2;
         const size_t lo = push_powers(wn, 1ull << lo_bits, nullptr);
         const Vec<NH> step = H.pow_u64(wn, 1ull << lo_bits);
@@ -372,8 +381,8 @@ struct PlanImpl final : PlanBase {
     if (hipMalloc(&d_tab, host.size() * 4) != hipSuccess ||
         hipMemcpy(d_tab, host.data(), host.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
       rc = NTT_ERR_HIP;
-    if (rc == NTT_OK && npass >= 2) rc = ensure_scratch(1);
-    if (rc == NTT_OK && npass >= 2) rc = build_full_tables();
+    if (rc == NTT_OK && npass >= 2 && !twiddle_only) rc = ensure_scratch(1);
+    if (rc == NTT_OK && npass >= 2 && !twiddle_only) rc = build_full_tables();
     hipSetDevice(cur);
     return rc;
   }
@@ -441,7 +450,7 @@ struct PlanImpl final : PlanBase {
   }
 
   int run(void* d, unsigned batch, bool inverse, hipStream_t st) override {
-    if (!d || batch == 0) return NTT_ERR_ARG;
+    if (!d || batch == 0 || (flags & NTT_PLAN_TWIDDLE_ONLY)) return NTT_ERR_ARG;
     if (log_n == 0) return NTT_OK;
     uint32_t* data = static_cast<uint32_t*>(d);
     const size_t* off_int = inverse ? off_int_i : off_int_f;
@@ -503,9 +512,28 @@ struct PlanImpl final : PlanBase {
     return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
   }
 
-  int fill(void* d, int kind, uint64_t seed, hipStream_t st) override {
+  int fill(void* d, uint64_t count, int kind, uint64_t seed, uint64_t row0, unsigned log_inner, unsigned log_stride,
+           hipStream_t st) override {
     if (!d || (kind != 0 && kind != 1)) return NTT_ERR_ARG;
-    hipError_t e = launch_fill<E>(kind, static_cast<uint32_t*>(d), n, seed, nrand, top_bits, st);
+    hipError_t e = launch_fill<E>(kind, static_cast<uint32_t*>(d), count, seed, nrand, top_bits, row0, log_inner,
+                                  log_stride, st);
+    return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+  }
+
+  int twiddle_pack(const void* src, void* dst, unsigned log_rows, unsigned log_len, unsigned log_bw, uint64_t row0,
+                   bool inverse, hipStream_t st) override {
+    if (!src || !dst || src == dst || log_bw > log_len || log_rows + log_len > 40) return NTT_ERR_ARG;
+    const uint32_t* lo = d_tab + (inverse ? off_lo_i : off_lo_f);
+    const uint32_t* hi = d_tab + (inverse ? off_hi_i : off_hi_f);
+    hipError_t e = launch_twiddle_pack<E>(static_cast<const uint32_t*>(src), static_cast<uint32_t*>(dst), log_rows,
+                                          log_len, log_bw, row0, log_n, lo, hi, lo_bits, inverse ? Fi : Ff, st);
+    return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+  }
+
+  int transpose(const void* src, void* dst, unsigned log_rows, unsigned log_cols, hipStream_t st) override {
+    if (!src || !dst || src == dst || log_rows + log_cols > 40) return NTT_ERR_ARG;
+    hipError_t e = launch_transpose<E>(static_cast<const uint32_t*>(src), static_cast<uint32_t*>(dst), log_rows,
+                                       log_cols, st);
     return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
   }
 };
@@ -522,7 +550,7 @@ static const FieldDef kFields[3] = {
 };
 
 static int make_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, const uint64_t* g64, unsigned limbs64,
-                     unsigned log_n, int device) {
+                     unsigned log_n, int device, unsigned flags) {
   if (log_n > 40) return NTT_ERR_ARG;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return NTT_ERR_NODEV;
@@ -538,15 +566,15 @@ static int make_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, const 
   if (limbs64 == 1) {
     if (p64[0] >= (1ull << 31)) return NTT_ERR_FIELD;  // `long long` path: 31-bit primes
     auto impl = std::make_unique<PlanImpl<EngP>>();
-    rc = impl->init(p32, g32, log_n, device);
+    rc = impl->init(p32, g32, log_n, device, flags);
     out = std::move(impl);
   } else if (limbs64 == 4) {
     auto impl = std::make_unique<PlanImpl<Eng256>>();
-    rc = impl->init(p32, g32, log_n, device);
+    rc = impl->init(p32, g32, log_n, device, flags);
     out = std::move(impl);
   } else if (limbs64 == 6) {
     auto impl = std::make_unique<PlanImpl<Eng384>>();
-    rc = impl->init(p32, g32, log_n, device);
+    rc = impl->init(p32, g32, log_n, device, flags);
     out = std::move(impl);
   } else {
     return NTT_ERR_ARG;
@@ -568,18 +596,27 @@ struct ntt_plan {
 
 extern "C" {
 
-int ntt_plan_create_custom(ntt_plan** out, const uint64_t* modulus, const uint64_t* generator, unsigned limbs64,
-                           unsigned log_n, int device) {
+int ntt_plan_create_custom_ex(ntt_plan** out, const uint64_t* modulus, const uint64_t* generator, unsigned limbs64,
+                              unsigned log_n, int device, unsigned flags) {
   if (!out || !modulus || !generator) return set_err(NTT_ERR_ARG);
   *out = nullptr;
   std::unique_ptr<PlanBase> impl;
-  int rc = make_plan(impl, modulus, generator, limbs64, log_n, device);
+  int rc = make_plan(impl, modulus, generator, limbs64, log_n, device, flags);
   if (rc != NTT_OK) return set_err(rc);
   *out = new ntt_plan{std::move(impl)};
   return set_err(NTT_OK);
 }
 
+int ntt_plan_create_custom(ntt_plan** out, const uint64_t* modulus, const uint64_t* generator, unsigned limbs64,
+                           unsigned log_n, int device) {
+  return ntt_plan_create_custom_ex(out, modulus, generator, limbs64, log_n, device, 0);
+}
+
 int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device) {
+  return ntt_plan_create_ex(out, field_id, log_n, limbs64, device, 0);
+}
+
+int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags) {
   if (field_id < 0 || field_id > 2) return set_err(NTT_ERR_ARG);
   if (limbs64 == 1 && field_id != NTT_FIELD_P469762049) return set_err(NTT_ERR_ARG);
   const FieldDef& F = kFields[field_id];
@@ -587,7 +624,7 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
   const unsigned L = limbs64 > 6 ? 6 : limbs64;
   for (unsigned i = 0; i < L && i < 4; ++i) p[i] = F.p[i];
   g[0] = F.g;
-  return ntt_plan_create_custom(out, p, g, limbs64, log_n, device);
+  return ntt_plan_create_custom_ex(out, p, g, limbs64, log_n, device, flags);
 }
 
 static int run_plan(ntt_plan* plan, void* d, unsigned batch, bool inv, void* stream) {
@@ -620,7 +657,25 @@ int ntt_polymul(ntt_plan* plan, void* a, void* b, void* c, void* s) {
 
 int ntt_fill(ntt_plan* plan, void* d, int kind, uint64_t seed, void* s) {
   if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
-  return set_err(plan->impl->fill(d, kind, seed, static_cast<hipStream_t>(s)));
+  return set_err(plan->impl->fill(d, plan->impl->n, kind, seed, 0, 64, 0, static_cast<hipStream_t>(s)));
+}
+
+int ntt_fill_map(ntt_plan* plan, void* d, uint64_t count, int kind, uint64_t seed, uint64_t row0, unsigned log_inner,
+                 unsigned log_stride, void* s) {
+  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
+  return set_err(plan->impl->fill(d, count, kind, seed, row0, log_inner, log_stride, static_cast<hipStream_t>(s)));
+}
+
+int ntt_twiddle_pack(ntt_plan* plan, const void* src, void* dst, unsigned log_rows, unsigned log_row_len,
+                     unsigned log_block, uint64_t row0, int inverse, void* s) {
+  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
+  return set_err(plan->impl->twiddle_pack(src, dst, log_rows, log_row_len, log_block, row0, inverse != 0,
+                                          static_cast<hipStream_t>(s)));
+}
+
+int ntt_transpose(ntt_plan* plan, const void* src, void* dst, unsigned log_rows, unsigned log_cols, void* s) {
+  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
+  return set_err(plan->impl->transpose(src, dst, log_rows, log_cols, static_cast<hipStream_t>(s)));
 }
 
 int ntt_plan_info(const ntt_plan* plan, uint64_t* n, unsigned* elem_bytes, unsigned* npasses, unsigned radix_log[8]) {

@@ -17,6 +17,7 @@ NTT_OK = 0
 NTT_FIELD_P469762049 = 0
 NTT_FIELD_BN254_FR = 1
 NTT_FIELD_BLS12_381_FR = 2
+NTT_PLAN_TWIDDLE_ONLY = 1
 
 # Every symbol declared in include/ntt.h with its ctypes prototype: (restype, argtypes).
 _vp = C.c_void_p
@@ -42,18 +43,12 @@ PROTOTYPES = {
                                C.c_uint32, C.c_uint32]),
     "NTT_GZKP_64": (C.c_int, [_vp, _vp, C.c_longlong, C.c_longlong, C.c_int, C.c_int, C.c_longlong]),
     "ntt_last_error": (C.c_int, []),
-    # multi-GPU (include/ntt_dist.h)
-    "ntt_dist_unique_id": (C.c_int, [C.c_char_p]),
-    "ntt_dist_comm_create": (C.c_int, [C.POINTER(_vp), C.c_char_p, C.c_int, C.c_int, C.c_int]),
-    "ntt_dist_comm_destroy": (C.c_int, [_vp]),
-    "ntt_dist_plan_create": (C.c_int, [C.POINTER(_vp), _vp, C.c_int, C.c_uint, C.c_uint]),
-    "ntt_dist_forward": (C.c_int, [_vp, _vp, _vp]),
-    "ntt_dist_inverse": (C.c_int, [_vp, _vp, _vp]),
-    "ntt_dist_pointwise_mul": (C.c_int, [_vp, _vp, _vp, _vp, _vp]),
-    "ntt_dist_info": (C.c_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint),
-                                C.POINTER(C.c_uint)]),
-    "ntt_dist_fill": (C.c_int, [_vp, _vp, C.c_int, C.c_uint64, _vp]),
-    "ntt_dist_plan_destroy": (C.c_int, [_vp]),
+    "ntt_plan_create_ex": (C.c_int, [C.POINTER(_vp), C.c_int, C.c_uint, C.c_uint, C.c_int, C.c_uint]),
+    "ntt_plan_create_custom_ex": (C.c_int, [C.POINTER(_vp), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_uint,
+                                            C.c_uint, C.c_int, C.c_uint]),
+    "ntt_fill_map": (C.c_int, [_vp, _vp, C.c_uint64, C.c_int, C.c_uint64, C.c_uint64, C.c_uint, C.c_uint, _vp]),
+    "ntt_twiddle_pack": (C.c_int, [_vp, _vp, _vp, C.c_uint, C.c_uint, C.c_uint, C.c_uint64, C.c_int, _vp]),
+    "ntt_transpose": (C.c_int, [_vp, _vp, _vp, C.c_uint, C.c_uint, _vp]),
 }
 
 _lock = threading.Lock()

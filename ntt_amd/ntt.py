@@ -78,7 +78,7 @@ class NTTPlan:
     """
 
     def __init__(self, field_id: int = 1, log_n: int = 10, limbs64: int = 4, device: int = 0,
-                 modulus: Optional[int] = None, generator: Optional[int] = None):
+                 modulus: Optional[int] = None, generator: Optional[int] = None, twiddle_only: bool = False):
         self._lib = _L.load()
         self.log_n = int(log_n)
         self.n = 1 << self.log_n
@@ -90,12 +90,13 @@ class NTTPlan:
         else:
             self.p, self.g = int(modulus), int(generator)
         h = C.c_void_p()
+        flags = _L.NTT_PLAN_TWIDDLE_ONLY if twiddle_only else 0
         if modulus is None:
-            st = self._lib.ntt_plan_create(C.byref(h), int(field_id), self.log_n, self.limbs64, self.device)
+            st = self._lib.ntt_plan_create_ex(C.byref(h), int(field_id), self.log_n, self.limbs64, self.device, flags)
         else:
-            st = self._lib.ntt_plan_create_custom(C.byref(h), _u64_array(int_to_limbs(self.p, self.limbs64)),
-                                                  _u64_array(int_to_limbs(self.g, self.limbs64)), self.limbs64,
-                                                  self.log_n, self.device)
+            st = self._lib.ntt_plan_create_custom_ex(C.byref(h), _u64_array(int_to_limbs(self.p, self.limbs64)),
+                                                     _u64_array(int_to_limbs(self.g, self.limbs64)), self.limbs64,
+                                                     self.log_n, self.device, flags)
         _L.check(st, "ntt_plan_create")
         self._h = h
         n = C.c_uint64()
@@ -168,6 +169,30 @@ class NTTPlan:
         _L.check(self._lib.ntt_fill(self._h, C.c_void_p(t.data_ptr()), k, int(seed), _stream_ptr(stream, t.device)),
                  "ntt_fill")
         return t
+
+    def fill_map(self, t: torch.Tensor, kind: str, seed: int, row0: int, log_inner: int, log_stride: int,
+                 stream=None) -> torch.Tensor:
+        """Local element i <- synthetic value of global j = row0 + (i >> log_inner) + ((i & m) << log_stride)."""
+        count = t.numel() * 8 // self.elem_bytes
+        k = {"iota": 0, "random": 1}[kind]
+        _L.check(self._lib.ntt_fill_map(self._h, C.c_void_p(t.data_ptr()), count, k, int(seed), int(row0),
+                                        int(log_inner), int(log_stride), _stream_ptr(stream, t.device)),
+                 "ntt_fill_map")
+        return t
+
+    def twiddle_pack(self, src: torch.Tensor, dst: torch.Tensor, log_rows: int, log_row_len: int, log_block: int,
+                     row0: int, inverse: bool = False, stream=None) -> torch.Tensor:
+        """dst[b >> log_block][a][b & m] = src[a][b] * w_n^(+-(row0 + a) * b) (four-step twiddle + pack)."""
+        _L.check(self._lib.ntt_twiddle_pack(self._h, C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()),
+                                            int(log_rows), int(log_row_len), int(log_block), int(row0),
+                                            int(bool(inverse)), _stream_ptr(stream, src.device)), "ntt_twiddle_pack")
+        return dst
+
+    def transpose(self, src: torch.Tensor, dst: torch.Tensor, log_rows: int, log_cols: int, stream=None):
+        _L.check(self._lib.ntt_transpose(self._h, C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()),
+                                         int(log_rows), int(log_cols), _stream_ptr(stream, src.device)),
+                 "ntt_transpose")
+        return dst
 
     def set_profiling(self, enable: bool = True) -> None:
         _L.check(self._lib.ntt_plan_set_profiling(self._h, int(bool(enable))), "ntt_plan_set_profiling")

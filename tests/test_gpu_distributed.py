@@ -1,0 +1,69 @@
+"""GPU checks of the multi-GPU four-step (ntt_amd.distributed) on a single MI355X:
+
+* G virtual ranks in one process (exchange = device copies), G = 1, 2, 4, 8: the gathered column
+  layout equals the single-GPU transform (itself checked against the oracle in test_gpu_parity),
+  and inverse(forward(x)) returns every rank's row-layout share;
+* a real torch.distributed (RCCL) process group of world size 1 through DistNTT.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _index(layout, kind):
+    i = torch.arange(layout.local_n, dtype=torch.int64, device="cuda:0")
+    if kind == "row":
+        a, j2 = i >> layout.log_n2, i & (layout.n2 - 1)
+        return layout.rank * layout.r + a + layout.n1 * j2
+    kc, k1 = i >> layout.log_n1, i & (layout.n1 - 1)
+    return layout.rank * layout.c + kc + layout.n2 * k1
+
+
+@pytest.mark.parametrize("world,log_n,field_id,L", [(1, 12, 1, 4), (2, 12, 1, 4), (4, 16, 1, 4), (8, 20, 1, 4),
+                                                     (8, 16, 2, 6), (2, 14, 0, 1)])
+def test_virtual_ranks_match_single_gpu(world, log_n, field_id, L):
+    from ntt_amd.distributed import VirtualRanks
+    from ntt_amd.ntt import NTTPlan
+    ref = NTTPlan(field_id, log_n, L)
+    x = ref.empty()
+    ref.fill(x, "random", seed=42)
+    x0 = x.clone()
+    ref.forward(x)
+    vr = VirtualRanks(field_id, log_n, L, world)
+    xs = vr.fill(vr.empty(), "random", seed=42)
+    for fs, t in zip(vr.ranks, xs):  # row-layout shares hold the right global elements
+        assert torch.equal(t, x0[_index(fs.L, "row")])
+    shares = [t.clone() for t in xs]
+    vr.forward(xs)
+    for fs, t in zip(vr.ranks, xs):
+        assert torch.equal(t, x[_index(fs.L, "col")]), (world, log_n, fs.L.rank)
+    vr.inverse(xs)
+    for s, t in zip(shares, xs):
+        assert torch.equal(s, t)
+
+
+def test_dist_ntt_rccl_world1():
+    import torch.distributed as dist
+    from ntt_amd.distributed import DistNTT
+    from ntt_amd.ntt import NTTPlan
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29561")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        log_n = 16
+        d = DistNTT(1, log_n, 4, device=0)
+        t = d.fill(d.empty(), "random", seed=3)
+        t0 = t.clone()
+        d.forward(t)
+        ref = NTTPlan(1, log_n, 4)
+        x = ref.fill(ref.empty(), "random", seed=3)
+        ref.forward(x)
+        assert torch.equal(t, x[_index(d.layout, "col")])
+        d.inverse(t)
+        assert torch.equal(t, t0)
+    finally:
+        dist.destroy_process_group()
