@@ -1,0 +1,54 @@
+"""Turn rocprofv3 --pmc CSVs (tools/profile_pmc.sh) into per-launch HBM traffic for bench.py.
+
+For the bench's NTT step, the kernel launches of one transform repeat in a fixed order (column
+passes, then the final pass).  Per-dispatch HBM bytes = 2 * FETCH_SIZE * 1024 (gfx950 reports half
+of a wide coalesced stream, MI355X_MICROARCH.md §HBM) + WRITE_SIZE * 1024, taken from the separate
+fetch and write passes and matched by dispatch order.  Writes profiles/pmc_summary.json:
+    {tag: [bytes of launch 0, launch 1, ...]}
+Usage: python tools/pmc_to_traffic.py gpurun_out/pmc TAG [profiles/pmc_summary.json]
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def per_dispatch(root, counter):
+    rows = defaultdict(float)
+    names = {}
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if (row.get("Counter_Name") or row.get("Counter-Name")) != counter:
+                continue
+            d = int(row.get("Dispatch_Id") or row.get("Dispatch-Id"))
+            rows[d] += float(row.get("Counter_Value") or row.get("Counter-Value") or 0)
+            names[d] = row.get("Kernel_Name") or row.get("Kernel-Name")
+    return [(names[d], rows[d]) for d in sorted(rows)]
+
+
+def main():
+    root, tag = sys.argv[1], sys.argv[2]
+    out = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_summary.json"
+    fetch = [(k, v) for k, v in per_dispatch(os.path.join(root, "fetch"), "FETCH_SIZE") if "k_pass" in k]
+    write = [(k, v) for k, v in per_dispatch(os.path.join(root, "write"), "WRITE_SIZE") if "k_pass" in k]
+    # launches per transform = number of distinct consecutive pass kernels at the tail
+    names = [k for k, _ in fetch]
+    per = 1
+    while per < len(names) and not ("KIND_FINAL" in names[per - 1] or ", 1, " in names[per - 1]):
+        per += 1
+    steps = len(fetch) // per
+    traffic = []
+    for i in range(per):
+        f = [fetch[s * per + i][1] for s in range(1, steps)] or [fetch[i][1]]
+        w = [write[s * per + i][1] for s in range(1, steps)] or [write[i][1]]
+        traffic.append(2 * 1024 * sum(f) / len(f) + 1024 * sum(w) / len(w))
+    d = json.load(open(out)) if os.path.exists(out) else {}
+    d[tag] = traffic
+    json.dump(d, open(out, "w"), indent=1)
+    print(tag, [f"{t / 1e9:.3f} GB" for t in traffic])
+
+
+if __name__ == "__main__":
+    main()
