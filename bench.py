@@ -3,12 +3,16 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 
-A "step" is one forward transform of the whole 2^24-element vector (SURVEY §8d synthetic vector B,
-SplitMix64 limbs), resident in HBM when the timed region starts.  N = 1: one MI355X
-(BASELINE configs[1]-class single-GPU workload at the headline size).  N > 1 (launched by
-torch.distributed.run, one rank per GPU): the SAME 2^24 transform distributed over N GPUs as a
-four-step with one RCCL all-to-all (strong scaling); `value` is always the whole-job
-rate n / t.
+A "step" is one forward transform of a whole 2^24-element vector (SURVEY §8d synthetic vector B,
+SplitMix64 limbs), resident in HBM when the timed region starts.
+
+* N = 1: one MI355X, one 2^24 transform per step.
+* N > 1 (torch.distributed.run, one rank per GPU): a 2^24 transform fits one GPU, and the
+  north star partitions the transform only from 2^26 up.  So every rank transforms its own 2^24
+  polynomial (different seeds), there is no data-path collective, and `value` = N * 2^24 / t with
+  t = max over ranks ("scaling": "weak").
+* --four-step: ONE transform of 2^log_n split over the N ranks with the RCCL all-to-all
+  (SURVEY §8e, strong scaling; e.g. BASELINE config 4: --four-step --log-n 28 on 8 GPUs).
 
 Rank 0 prints one JSON line with `roofline` (HBM roofline of the dominant kernel, measured with
 HIP events on its launch stream inside the timed region) and `cpu_baseline` (the C oracle on the
@@ -41,7 +45,8 @@ def parse():
     ap.add_argument("--limbs", type=int, default=4)
     ap.add_argument("--inverse", action="store_true", help="time the inverse instead of the forward")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--dist", action="store_true", help="use the distributed four-step even at world size 1")
+    ap.add_argument("--four-step", "--dist", dest="four_step", action="store_true",
+                    help="one transform split over all ranks (four-step + RCCL all-to-all)")
     ap.add_argument("--cpu-log-n", type=int, default=22, help="C-oracle sample size (log2)")
     return ap.parse_args()
 
@@ -86,13 +91,14 @@ def main():
     torch.cuda.set_device(local)
     n = 1 << args.log_n
 
-    use_dist = world > 1 or args.dist
+    use_dist = world > 1 or args.four_step
     if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29512")
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    if args.four_step:
         from ntt_amd.distributed import DistNTT
         eng = DistNTT(field_id=args.field, log_n=args.log_n, limbs64=args.limbs, device=local)
         data = eng.empty()
@@ -103,7 +109,7 @@ def main():
         from ntt_amd.ntt import NTTPlan
         plan = NTTPlan(field_id=args.field, log_n=args.log_n, limbs64=args.limbs, device=local)
         data = plan.empty()
-        plan.fill(data, "random", seed=2)
+        plan.fill(data, "random", seed=2 + rank)  # each rank its own polynomial
         step = (lambda: plan.inverse(data)) if args.inverse else (lambda: plan.forward(data))
         plan_for_prof = plan
 
@@ -135,7 +141,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms_per_step = elapsed / args.steps * 1e3
-    value = n / (elapsed / args.steps)
+    jobs = 1 if args.four_step else world  # independent 2^log_n transforms per step
+    value = jobs * n / (elapsed / args.steps)
 
     elem_bytes = 8 if args.limbs == 1 else 8 * args.limbs
     passes = list(getattr(plan_for_prof, "passes", []))
@@ -150,7 +157,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "strong" if args.four_step else "weak",
         "vs_baseline": None,
         "dtype": "uint256 (8x32-bit limbs, Montgomery)" if args.limbs == 4 else
                  ("uint384 (12x32-bit limbs, Montgomery)" if args.limbs == 6 else "uint32 Montgomery"),
@@ -159,13 +166,16 @@ def main():
                                f"{FIELD_NAMES[args.field]}, {args.limbs}x64-bit limbs, natural order, in place",
                    "log_n": args.log_n, "field": FIELD_NAMES[args.field], "limbs64": args.limbs,
                    "passes_log_radix": passes,
-                   "parallelism": "single GPU" if not use_dist else f"four-step over {world} GPU(s) (RCCL all-to-all)"},
+                   "parallelism": (f"four-step over {world} GPU(s) (RCCL all-to-all)" if args.four_step else
+                                   ("single GPU" if world == 1 else
+                                    f"{world} GPUs, one independent transform per rank (no data-path collective)")),
+                   "transforms_per_step": jobs},
     }
     if launch_avg:
         # dominant kernel = the longest launch; algorithmic bytes per launch = one read + one write
         # of the local vector (2*n*S per pass over all n elements).
         k = max(range(len(launch_avg)), key=lambda i: launch_avg[i])
-        local_n = n // world
+        local_n = n // world if args.four_step else n
         alg_bytes = 2 * local_n * elem_bytes
         achieved = alg_bytes / (launch_avg[k] * 1e-3) / 1e9
         tag = f"f{args.field}_L{args.limbs}_n{args.log_n}_w{world}"
@@ -176,8 +186,8 @@ def main():
                            "kernel": f"launch {k} of {len(launch_avg)}", "kernel_ms": launch_avg[k],
                            "algorithmic_bytes_per_launch": alg_bytes,
                            "launch_ms": launch_avg}
-        total_alg = 2 * n * elem_bytes * max(1, len(launch_avg))
-        out["hbm_effective_gbps_whole_transform"] = total_alg / world / (ms_per_step * 1e-3) / 1e9
+        total_alg = 2 * local_n * elem_bytes * max(1, len(launch_avg))
+        out["hbm_effective_gbps_per_gpu"] = total_alg / (ms_per_step * 1e-3) / 1e9
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args.field, args.limbs if args.limbs != 1 else 1, args.cpu_log_n)
