@@ -18,7 +18,9 @@ BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libntt.so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
-SOURCES = ["ntt_k8.hip", "ntt_k12.hip", "ntt_k1.hip", "ntt_plan.cpp"]
+# slowest translation units first (the pool runs them in list order)
+SOURCES = [f"ntt_{e}_{k}.hip" for e in ("e384", "e256", "ep") for k in ("col", "single", "fin", "misc")]
+SOURCES.append("ntt_plan.cpp")
 ARCH = os.environ.get("NTT_OFFLOAD_ARCH", "gfx950")
 
 

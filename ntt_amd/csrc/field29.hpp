@@ -115,6 +115,83 @@ F29_HD void mont29(uint32_t (&r)[L], const uint32_t (&a)[L], const uint32_t (&b)
   }
 }
 
+// ---------------------------------------------------------------- single-chain MAD helpers
+// v_mad_u64_u32 through inline asm: the compiler cannot split a column's accumulation into two
+// chains re-joined by a 64-bit add (it does for the plain C++ form: +17 v_lshl_add_u64 per product).
+// mad29v: both factors per-lane (VGPR); mad29s: b wave-uniform (an SGPR, e.g. the modulus).
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ uint64_t mad29v(uint32_t a, uint32_t b, uint64_t c) {
+  uint64_t r, cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cc) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ uint64_t mad29s(uint32_t a, uint32_t b, uint64_t c) {
+  uint64_t r, cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cc) : "v"(a), "s"(b), "v"(c));
+  return r;
+}
+#else
+static inline uint64_t mad29v(uint32_t a, uint32_t b, uint64_t c) { return c + (uint64_t)a * b; }
+static inline uint64_t mad29s(uint32_t a, uint32_t b, uint64_t c) { return c + (uint64_t)a * b; }
+#endif
+
+// mont29 with every column accumulated in ONE dependent chain (same result as mont29).
+template <int L>
+F29_HD void mont29_chain(uint32_t (&r)[L], const uint32_t (&a)[L], const uint32_t (&b)[L], const Mod29<L>& M) {
+  uint32_t m[L];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+#pragma unroll
+    for (int j = 0; j <= i; ++j) acc = mad29v(a[j], b[i - j], acc);
+#pragma unroll
+    for (int j = 0; j < i; ++j) acc = mad29s(m[j], M.p[i - j], acc);
+    m[i] = ((uint32_t)acc * M.pinv) & kMask29;
+    acc = mad29s(m[i], M.p[0], acc);
+    acc >>= 29;
+  }
+#pragma unroll
+  for (int i = L; i < 2 * L; ++i) {
+#pragma unroll
+    for (int j = i - L + 1; j < L; ++j) acc = mad29v(a[j], b[i - j], acc);
+#pragma unroll
+    for (int j = i - L + 1; j < L; ++j) acc = mad29s(m[j], M.p[i - j], acc);
+    r[i - L] = (uint32_t)acc & kMask29;
+    acc >>= 29;
+  }
+}
+
+// Multiplication by a precomputed constant (Shoup): w < p, ws = floor(w * B / p), B = 2^(29L),
+// pbar = B - p (normalised limbs).  q = floor(x * ws / B) is formed from columns >= L-2 of x*ws
+// only (the dropped columns sum to < B for x limbs < 2^31, so q is short by at most 1), and
+// r = x*w - q*p = (x*w + q*pbar) mod B lies in [0, 3p) for ANY x < B.  143 MADs for L = 9
+// (53 + 90) versus 162 for the Montgomery product, and no m = t * pinv multiplies.
+template <int L>
+F29_HD void mulc29(uint32_t (&r)[L], const uint32_t (&x)[L], const uint32_t (&w)[L], const uint32_t (&ws)[L],
+                   const uint32_t (&pbar)[L]) {
+  uint32_t q[L];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = L - 2; k < 2 * L - 1; ++k) {
+#pragma unroll
+    for (int i = (k - (L - 1) > 0 ? k - (L - 1) : 0); i <= (k < L - 1 ? k : L - 1); ++i)
+      acc = mad29v(x[i], ws[k - i], acc);
+    if (k >= L) q[k - L] = (uint32_t)acc & kMask29;
+    acc >>= 29;
+  }
+  q[L - 1] = (uint32_t)acc;
+  acc = 0;
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+#pragma unroll
+    for (int i = 0; i <= k; ++i) acc = mad29v(x[i], w[k - i], acc);
+#pragma unroll
+    for (int i = 0; i <= k; ++i) acc = mad29s(q[i], pbar[k - i], acc);
+    r[k] = (uint32_t)acc & kMask29;
+    acc >>= 29;
+  }
+}
+
 // ---------------------------------------------------------------- 32-bit <-> 29-bit limb packing
 // canonical little-endian 32-bit words (W32 of them) -> L normalised 29-bit limbs
 template <int L, int W32>

@@ -1,0 +1,5 @@
+// Eng384: k_pass instantiations for KIND_COLUMN.
+#include "ntt_kernels_impl.hpp"
+namespace ntt {
+NTT_INSTANTIATE_KIND(Eng384, KIND_COLUMN)
+}  // namespace ntt

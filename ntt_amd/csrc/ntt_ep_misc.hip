@@ -1,4 +1,4 @@
-// Explicit instantiation of the NTT kernels for the EngP engine.
+// EngP: launchers, fill / pack / transpose / pointwise / twiddle-build kernels.
 #include "ntt_kernels_impl.hpp"
 namespace ntt {
 NTT_INSTANTIATE(EngP)

@@ -1,0 +1,5 @@
+// EngP: k_pass instantiations for KIND_SINGLE.
+#include "ntt_kernels_impl.hpp"
+namespace ntt {
+NTT_INSTANTIATE_KIND(EngP, KIND_SINGLE)
+}  // namespace ntt

@@ -36,6 +36,9 @@ struct PassArgs {
   size_t batch_stride;   // 32-bit words between batched transforms
 };
 
+template <class E, int KIND>
+hipError_t launch_pass_kind(int logr, const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t grid,
+                            uint32_t batch, hipStream_t st);
 template <class E>
 hipError_t launch_pass(int kind, int logr, const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t grid,
                        uint32_t batch, hipStream_t st);

@@ -304,6 +304,7 @@ __global__ void k_dft_naive(const uint32_t* __restrict__ src, uint32_t* __restri
     E::load(acc, src + boff, 0);
     E::tload(w, A.tw_int, 0);
     E::mul(acc, w, A.F);
+#pragma unroll 1
     for (uint32_t j = 1; j < n; ++j) {
       E::load(v, src + boff, j);
       E::tload(w, A.tw_int, (j * k) & (n - 1));
@@ -515,7 +516,7 @@ static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassAr
 }
 
 template <class E, int KIND>
-static hipError_t launch_pass_k(int logr, const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t grid,
+hipError_t launch_pass_kind(int logr, const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t grid,
                                 uint32_t batch, hipStream_t st) {
   switch (logr) {
     case 3: return launch_pass_r<E, KIND, 3>(src, dst, A, grid, batch, st);
@@ -534,9 +535,9 @@ static hipError_t launch_pass_k(int logr, const uint32_t* src, uint32_t* dst, co
 template <class E>
 hipError_t launch_pass(int kind, int logr, const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t grid,
                        uint32_t batch, hipStream_t st) {
-  if (kind == KIND_COLUMN) return launch_pass_k<E, KIND_COLUMN>(logr, src, dst, A, grid, batch, st);
-  if (kind == KIND_FINAL) return launch_pass_k<E, KIND_FINAL>(logr, src, dst, A, grid, batch, st);
-  return launch_pass_k<E, KIND_SINGLE>(logr, src, dst, A, grid, batch, st);
+  if (kind == KIND_COLUMN) return launch_pass_kind<E, KIND_COLUMN>(logr, src, dst, A, grid, batch, st);
+  if (kind == KIND_FINAL) return launch_pass_kind<E, KIND_FINAL>(logr, src, dst, A, grid, batch, st);
+  return launch_pass_kind<E, KIND_SINGLE>(logr, src, dst, A, grid, batch, st);
 }
 
 template <class E>
@@ -565,7 +566,19 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
   return hipGetLastError();
 }
 
+// One pass kind of one engine per translation unit (the kernels dominate compile time).
+#define NTT_INSTANTIATE_KIND(E, KIND)                                                                          \
+  template hipError_t launch_pass_kind<E, KIND>(int, const uint32_t*, uint32_t*, const PassArgs<E>&, uint32_t, \
+                                                uint32_t, hipStream_t);
+
+#define NTT_EXTERN_KIND(E, KIND)                                                                                     \
+  extern template hipError_t launch_pass_kind<E, KIND>(int, const uint32_t*, uint32_t*, const PassArgs<E>&, uint32_t, \
+                                                       uint32_t, hipStream_t);
+
 #define NTT_INSTANTIATE(E)                                                                                         \
+  NTT_EXTERN_KIND(E, KIND_COLUMN)                                                                                  \
+  NTT_EXTERN_KIND(E, KIND_FINAL)                                                                                   \
+  NTT_EXTERN_KIND(E, KIND_SINGLE)                                                                                  \
   template hipError_t launch_pass<E>(int, int, const uint32_t*, uint32_t*, const PassArgs<E>&, uint32_t, uint32_t, \
                                      hipStream_t);                                                                 \
   template hipError_t launch_naive<E>(const uint32_t*, uint32_t*, const PassArgs<E>&, uint32_t, hipStream_t);       \
