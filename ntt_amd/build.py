@@ -14,8 +14,12 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-BUILD = os.path.join(HERE, "_build")
-LIB = os.path.join(HERE, "libntt.so")
+# Experiment variants (never the default product): NTT_BUILD_TAG=<tag> NTT_BUILD_DEFINES="-DX=1 ..."
+# builds ntt_amd/libntt_<tag>.so from ntt_amd/_build_<tag>/; NTT_LIB_PATH selects it at load time.
+_TAG = os.environ.get("NTT_BUILD_TAG", "")
+_DEFINES = os.environ.get("NTT_BUILD_DEFINES", "").split()
+BUILD = os.path.join(HERE, "_build" + (f"_{_TAG}" if _TAG else ""))
+LIB = os.path.join(HERE, "libntt" + (f"_{_TAG}" if _TAG else "") + ".so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
 # slowest translation units first (the pool runs them in list order)
@@ -46,7 +50,7 @@ def _compile(src: str, hdr_mtime: float) -> str:
     if os.path.exists(o) and os.path.getmtime(o) >= max(os.path.getmtime(s), hdr_mtime):
         return o
     cmd = [hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-c", s, "-o", o,
-           "-I", CSRC, "-I", INCLUDE, "-Wno-pass-failed", "-Wno-unused-command-line-argument"]
+           "-I", CSRC, "-I", INCLUDE, "-Wno-pass-failed", "-Wno-unused-command-line-argument", *_DEFINES]
     if src.endswith(".cpp"):
         cmd[1:1] = ["-x", "hip"]
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -9,21 +9,45 @@
 #pragma once
 #include "field.hpp"
 #include "field29.hpp"
+#include "field29_asm9.hpp"
+
+#ifndef NTT_WAVES_256
+#define NTT_WAVES_256 2
+#endif
 
 namespace ntt {
 
 // ------------------------------------------------------------------------------ 29-bit engine
+// Twiddles are multiplied with Shoup's precomputed-quotient product (mulc29): a table entry holds
+// the canonical w and ws = floor(w * B / p), B = 2^(29L).  143 MADs per product for L = 9 instead
+// of the Montgomery product's 162, measured 14-18 % faster per product on MI355X
+// (profiles/r01_mb_mont29_v2.txt).  Element x twiddle products are < 3p for any input < B.
+//
+// Lazy bounds (units of p): the in-register DFTs take inputs < IN p (IN = 4: products < 3p,
+// reduced k = 0 outputs < 4p, HBM loads < p) and radix-2 stage s adds/subtracts with offset
+// IN 2^(s-1) p, so a Q-point DFT returns values < IN Q p <= 32p < B for every supported field.
 template <int L, int W32>
 struct Eng29 {
-  static constexpr int W = L;               // registers per element
-  static constexpr int MEMW = W32;          // 32-bit words per element in HBM
-  static constexpr int TW = (L + 3) & ~3;   // words per twiddle-table entry (16-B aligned)
-  static constexpr int LDSW = L;            // words per element in LDS
+  static constexpr int W = L;                   // registers per element
+  static constexpr int MEMW = W32;              // 32-bit words per element in HBM (canonical)
+  static constexpr int TW = (2 * L + 3) & ~3;   // words per twiddle-table entry: w, ws (16-B aligned)
+  static constexpr int LDSW = L;                // words per element in LDS
+  static constexpr int IN = 4;                  // DFT input bound (units of p)
+  static constexpr int MUL_OUT = 4;             // bound used for twiddle products (they are < 3p)
+  // pass-kernel occupancy target: 2 waves/SIMD (<= 256 VGPRs).  3 waves (<= 168 VGPRs, split LDS
+  // exchanges) spills ~300 B/thread with the Shoup operands live and measured 15 % slower.
+  static constexpr int WAVES_PER_EU = (L <= 9) ? NTT_WAVES_256 : 2;
+  static constexpr bool LDS_SPLIT = WAVES_PER_EU >= 3;
+  struct Tw {
+    uint32_t w[L];   // canonical twiddle
+    uint32_t ws[L];  // floor(w * B / p)
+  };
   struct Args {
-    Mod29<L> M;
-    uint32_t p4[L], p8[L];  // 4p, 8p (normalised) for the lazy butterflies
-    uint32_t w8[3][L];  // w_8^1, w_8^2, w_8^3 (Montgomery, R = 2^(29L))
-    uint32_t ninv[L];   // n^-1 (Montgomery)
+    Mod29<L> M;           // p, 2p, -p^-1 mod 2^29 (Montgomery products of two variables)
+    uint32_t kp[5][L];    // 2^j p, j = 0..4, normalised: lazy offsets and reductions
+    uint32_t pbar[L];     // B - p (Shoup)
+    Tw w8[3];             // w_8^1, w_8^2, w_8^3
+    Tw ninv;              // n^-1
   };
 
   __device__ static __forceinline__ void load(uint32_t (&x)[W], const uint32_t* __restrict__ base, size_t idx) {
@@ -36,48 +60,63 @@ struct Eng29 {
     }
     pack29<L, W32>(x, w);
   }
-  // x < 2p -> canonical -> HBM
+  // x < FROM p (power of two) -> x < TO p by conditional subtractions of FROM/2 p, ..., TO p
+  template <int FROM, int TO>
+  __device__ static __forceinline__ void reduce(uint32_t (&x)[W], const Args& A) {
+    static_assert(FROM <= 32 && TO >= 1, "lazy bound");
+    if constexpr (FROM > TO) {
+      constexpr int j = __builtin_ctz(FROM / 2);
+      cond_sub<L>(x, A.kp[j]);
+      reduce<FROM / 2, TO>(x, A);
+    }
+  }
+  // x < BOUND p -> canonical -> HBM
+  template <int BOUND>
   __device__ static __forceinline__ void store(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
                                                const Args& A) {
-    cond_sub<L>(x, A.M.p);
+    reduce<BOUND, 1>(x, A);
     uint32_t w[W32];
     unpack29<L, W32>(w, x);
     uint4* p = reinterpret_cast<uint4*>(base + idx * W32);
 #pragma unroll
     for (int q = 0; q < W32 / 4; ++q) p[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
   }
-  __device__ static __forceinline__ void tload(uint32_t (&x)[W], const uint32_t* __restrict__ tab, uint32_t idx) {
-    const uint4* p = reinterpret_cast<const uint4*>(tab + (size_t)idx * TW);
+  __device__ static __forceinline__ void tload(Tw& t, const uint32_t* __restrict__ tab, size_t idx) {
+    const uint4* p = reinterpret_cast<const uint4*>(tab + idx * TW);
 #pragma unroll
     for (int q = 0; q < TW / 4; ++q) {
       const uint4 v = p[q];
-      if (4 * q + 0 < L) x[4 * q + 0] = v.x;
-      if (4 * q + 1 < L) x[4 * q + 1] = v.y;
-      if (4 * q + 2 < L) x[4 * q + 2] = v.z;
-      if (4 * q + 3 < L) x[4 * q + 3] = v.w;
+      const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 4 * q + r;
+        if (i < L) t.w[i] = vv[r];
+        else if (i < 2 * L) t.ws[i - L] = vv[r];
+      }
     }
   }
-  __device__ static __forceinline__ void mul(uint32_t (&x)[W], const uint32_t (&w)[W], const Args& A) {
+  // x <- x * w mod p, x any value < B (limbs < 2^31): result < 3p
+  __device__ static __forceinline__ void mul(uint32_t (&x)[W], const Tw& t, const Args& A) {
     uint32_t r[W];
-    mont29<L>(r, x, w, A.M);
+    if constexpr (L == 9)
+      mulc29_a9(r, x, t.w, t.ws, A.pbar);
+    else
+      mulc29_blk<L>(r, x, t.w, t.ws, A.pbar);
 #pragma unroll
     for (int i = 0; i < W; ++i) x[i] = r[i];
   }
-  // ---- lazy DIF butterflies for the in-register DFTs: stage s (1-based) takes inputs < 2^s p and
-  // produces (a + b, a - b + K p) with K = 2^s, i.e. outputs < 2^(s+1) p.  Sums and differences are
-  // only carry-normalised (no conditional subtraction); values stay far below R = 2^(29L) (16p <
-  // 2^259), so every Montgomery product still returns < 2p.  reduce_to_2p() brings the outputs that
-  // are not multiplied afterwards back under 2p.
-  template <int K>
-  __device__ static __forceinline__ const uint32_t (&kp(const Args& A))[L] {
-    static_assert(K == 2 || K == 4 || K == 8, "lazy bound");
-    if constexpr (K == 2) return A.M.p2;
-    else if constexpr (K == 4) return A.p4;
-    else return A.p8;
+  // x <- x * y / B mod p (Montgomery product of two variables), x < 32p, y < 4p: result < 3p
+  __device__ static __forceinline__ void mulv(uint32_t (&x)[W], const uint32_t (&y)[W], const Args& A) {
+    uint32_t r[W];
+    if constexpr (L == 9)
+      mont29_a9(r, x, y, A.M);
+    else
+      mont29<L>(r, x, y, A.M);
+#pragma unroll
+    for (int i = 0; i < W; ++i) x[i] = r[i];
   }
-  template <int K>
-  __device__ static __forceinline__ void bfly_l(uint32_t (&a)[W], uint32_t (&b)[W], const Args& A) {
-    const uint32_t(&q)[L] = kp<K>(A);
+  // ---- lazy DIF butterflies: a, b < K p  ->  (a + b, a - b + K p), both < 2K p, normalised.
+  __device__ static __forceinline__ void bfly_lk(uint32_t (&a)[W], uint32_t (&b)[W], const uint32_t (&q)[L]) {
 #pragma unroll
     for (int i = 0; i < L; ++i) {
       const uint32_t x = a[i], y = b[i];
@@ -88,54 +127,39 @@ struct Eng29 {
     norm_s<L>(b);
   }
   template <int K>
-  __device__ static __forceinline__ void bfly_w_l(uint32_t (&a)[W], uint32_t (&b)[W], const uint32_t (&w)[W],
+  __device__ static __forceinline__ void bfly_l(uint32_t (&a)[W], uint32_t (&b)[W], const Args& A) {
+    static_assert(K == 4 || K == 8 || K == 16, "lazy bound");
+    bfly_lk(a, b, A.kp[__builtin_ctz(K)]);
+  }
+  template <int K>
+  __device__ static __forceinline__ void bfly_w_l(uint32_t (&a)[W], uint32_t (&b)[W], const Tw& t,
                                                   const Args& A) {
     bfly_l<K>(a, b, A);
-    uint32_t r[W];
-    mont29<L>(r, b, w, A.M);
-#pragma unroll
-    for (int i = 0; i < W; ++i) b[i] = r[i];
-  }
-  // x < B p -> x < 2p (B a power of two <= 16)
-  template <int B>
-  __device__ static __forceinline__ void reduce_to_2p(uint32_t (&x)[W], const Args& A) {
-    if constexpr (B > 8) cond_sub<L>(x, A.p8);
-    if constexpr (B > 4) cond_sub<L>(x, A.p4);
-    if constexpr (B > 2) cond_sub<L>(x, A.M.p2);
-  }
-
-  // DIF butterflies on lazy residues (< 2p in, < 2p out)
-  __device__ static __forceinline__ void bfly(uint32_t (&a)[W], uint32_t (&b)[W], const Args& A) {
-    uint32_t u[W], d[W];
-    add29<L>(u, a, b, A.M);
-    sub29<L>(d, a, b, A.M);
-#pragma unroll
-    for (int i = 0; i < W; ++i) { a[i] = u[i]; b[i] = d[i]; }
-  }
-  __device__ static __forceinline__ void bfly_w(uint32_t (&a)[W], uint32_t (&b)[W], const uint32_t (&w)[W],
-                                                const Args& A) {
-    uint32_t u[W], d[W];
-    add29<L>(u, a, b, A.M);
-    sub29_raw<L>(d, a, b, A.M);  // < 4p, fine as a Montgomery operand
-    mont29<L>(b, d, w, A.M);
-#pragma unroll
-    for (int i = 0; i < W; ++i) a[i] = u[i];
+    mul(b, t, A);
   }
 };
 
 // ------------------------------------------------------------------------------ 32-bit engine
 // N x 32-bit limbs, canonical residues, CIOS/FIPS Montgomery (field.hpp).  Used for the 1-limb
-// P469762049 `long long` path (MEMW = 2).
+// P469762049 `long long` path (MEMW = 2).  Twiddles are stored in Montgomery form (w R), so
+// mont_mul(x, w R) = x w; every value stays canonical and the lazy-bound parameters are ignored.
 template <int N, int MEMW_>
 struct Eng32 {
   static constexpr int W = N;
   static constexpr int MEMW = MEMW_;
   static constexpr int TW = N;
   static constexpr int LDSW = N;
+  static constexpr int IN = 4;
+  static constexpr int MUL_OUT = 4;
+  static constexpr int WAVES_PER_EU = 4;
+  static constexpr bool LDS_SPLIT = false;
+  struct Tw {
+    uint32_t w[N];  // w R mod p
+  };
   struct Args {
     Modulus<N> M;
-    uint32_t w8[3][N];
-    uint32_t ninv[N];
+    Tw w8[3];
+    Tw ninv;
   };
   __device__ static __forceinline__ void load(uint32_t (&x)[W], const uint32_t* __restrict__ base, size_t idx) {
     if constexpr (N == 1) {
@@ -149,6 +173,9 @@ struct Eng32 {
       }
     }
   }
+  template <int FROM, int TO>
+  __device__ static __forceinline__ void reduce(uint32_t (&)[W], const Args&) {}
+  template <int BOUND>
   __device__ static __forceinline__ void store(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
                                                const Args&) {
     if constexpr (N == 1) {
@@ -159,67 +186,78 @@ struct Eng32 {
       for (int q = 0; q < N / 4; ++q) p[q] = make_uint4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
     }
   }
-  __device__ static __forceinline__ void tload(uint32_t (&x)[W], const uint32_t* __restrict__ tab, uint32_t idx) {
+  __device__ static __forceinline__ void tload(Tw& t, const uint32_t* __restrict__ tab, size_t idx) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) x[i] = tab[(size_t)idx * N + i];
+    for (int i = 0; i < N; ++i) t.w[i] = tab[idx * N + i];
   }
-  __device__ static __forceinline__ void mul(uint32_t (&x)[W], const uint32_t (&w)[W], const Args& A) {
-    mont_mul<N>(x, x, w, A.M);
+  __device__ static __forceinline__ void mul(uint32_t (&x)[W], const Tw& t, const Args& A) {
+    mont_mul<N>(x, x, t.w, A.M);
+  }
+  __device__ static __forceinline__ void mulv(uint32_t (&x)[W], const uint32_t (&y)[W], const Args& A) {
+    mont_mul<N>(x, x, y, A.M);
   }
   template <int K>
   __device__ static __forceinline__ void bfly_l(uint32_t (&a)[W], uint32_t (&b)[W], const Args& A) {
-    bfly(a, b, A);
-  }
-  template <int K>
-  __device__ static __forceinline__ void bfly_w_l(uint32_t (&a)[W], uint32_t (&b)[W], const uint32_t (&w)[W],
-                                                  const Args& A) {
-    bfly_w(a, b, w, A);
-  }
-  template <int B>
-  __device__ static __forceinline__ void reduce_to_2p(uint32_t (&)[W], const Args&) {}
-  __device__ static __forceinline__ void bfly(uint32_t (&a)[W], uint32_t (&b)[W], const Args& A) {
     uint32_t s[W], d[W];
     add_mod<N>(s, a, b, A.M);
     sub_mod<N>(d, a, b, A.M);
 #pragma unroll
     for (int i = 0; i < W; ++i) { a[i] = s[i]; b[i] = d[i]; }
   }
-  __device__ static __forceinline__ void bfly_w(uint32_t (&a)[W], uint32_t (&b)[W], const uint32_t (&w)[W],
-                                                const Args& A) {
-    uint32_t s[W], d[W];
-    add_mod<N>(s, a, b, A.M);
-    sub_mod<N>(d, a, b, A.M);
-#pragma unroll
-    for (int i = 0; i < W; ++i) a[i] = s[i];
-    mont_mul<N>(b, d, w, A.M);
+  template <int K>
+  __device__ static __forceinline__ void bfly_w_l(uint32_t (&a)[W], uint32_t (&b)[W], const Tw& t,
+                                                  const Args& A) {
+    bfly_l<K>(a, b, A);
+    mont_mul<N>(b, b, t.w, A.M);
   }
 };
 
 // ------------------------------------------------------------------------------ LDS (any engine)
 // An element of LDSW words is split into 16-byte planes ([plane][idx]) plus a 4-byte plane per
 // leftover word, so lanes reading consecutive indices hit consecutive slots.
-template <int LDSW, int E>
-__device__ __forceinline__ void lds_put(uint32_t* lds, uint32_t idx, const uint32_t (&x)[LDSW]) {
-  constexpr int Q = LDSW / 4;
+//
+// With SPLIT (engines that target 3 waves/SIMD) exchanges run in two rounds over the same buffer:
+// part 0 moves planes [0, Q/2) and the leftover words, part 1 planes [Q/2, Q).  Halving the words
+// resident at once halves the tile's LDS (40 KiB instead of 72 KiB for a 2048-element 256-bit
+// tile), which lets 3 workgroups (3 waves per SIMD) share a CU instead of 2.
+template <int LDSW, bool SPLIT>
+struct LdsParts {
+  static constexpr int Q = LDSW / 4, REM = LDSW - 4 * Q;
+  static constexpr int PARTS = (SPLIT && Q >= 2) ? 2 : 1;
+  static constexpr int q_lo(int part) { return PARTS == 1 ? 0 : (part == 0 ? 0 : Q / 2); }
+  static constexpr int q_hi(int part) { return PARTS == 1 ? Q : (part == 0 ? Q / 2 : Q); }
+  static constexpr bool has_rem(int part) { return part == 0; }
+  static constexpr int words(int part) { return 4 * (q_hi(part) - q_lo(part)) + (has_rem(part) ? REM : 0); }
+  static constexpr int max_words() { return words(0) > words(PARTS - 1) ? words(0) : words(PARTS - 1); }
+};
+
+template <int LDSW, bool SPLIT, int E, int PART>
+__device__ __forceinline__ void lds_put_part(uint32_t* lds, uint32_t idx, const uint32_t (&x)[LDSW]) {
+  using P = LdsParts<LDSW, SPLIT>;
   uint4* l4 = reinterpret_cast<uint4*>(lds);
 #pragma unroll
-  for (int q = 0; q < Q; ++q) l4[q * E + idx] = make_uint4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
-  uint32_t* l1 = lds + 4 * Q * E;
+  for (int q = P::q_lo(PART); q < P::q_hi(PART); ++q)
+    l4[(q - P::q_lo(PART)) * E + idx] = make_uint4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+  if constexpr (P::has_rem(PART)) {
+    uint32_t* l1 = lds + 4 * (P::q_hi(PART) - P::q_lo(PART)) * E;
 #pragma unroll
-  for (int r = 4 * Q; r < LDSW; ++r) l1[(r - 4 * Q) * E + idx] = x[r];
+    for (int r = 4 * P::Q; r < LDSW; ++r) l1[(r - 4 * P::Q) * E + idx] = x[r];
+  }
 }
-template <int LDSW, int E>
-__device__ __forceinline__ void lds_get(uint32_t (&x)[LDSW], const uint32_t* lds, uint32_t idx) {
-  constexpr int Q = LDSW / 4;
+template <int LDSW, bool SPLIT, int E, int PART>
+__device__ __forceinline__ void lds_get_part(uint32_t (&x)[LDSW], const uint32_t* lds, uint32_t idx) {
+  using P = LdsParts<LDSW, SPLIT>;
   const uint4* l4 = reinterpret_cast<const uint4*>(lds);
 #pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const uint4 v = l4[q * E + idx];
+  for (int q = P::q_lo(PART); q < P::q_hi(PART); ++q) {
+    const uint4 v = l4[(q - P::q_lo(PART)) * E + idx];
     x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
   }
-  const uint32_t* l1 = lds + 4 * Q * E;
+  if constexpr (P::has_rem(PART)) {
+    const uint32_t* l1 = lds + 4 * (P::q_hi(PART) - P::q_lo(PART)) * E;
 #pragma unroll
-  for (int r = 4 * Q; r < LDSW; ++r) x[r] = l1[(r - 4 * Q) * E + idx];
+    for (int r = 4 * P::Q; r < LDSW; ++r) x[r] = l1[(r - 4 * P::Q) * E + idx];
+  }
 }
 
 }  // namespace ntt

@@ -135,6 +135,121 @@ static inline uint64_t mad29v(uint32_t a, uint32_t b, uint64_t c) { return c + (
 static inline uint64_t mad29s(uint32_t a, uint32_t b, uint64_t c) { return c + (uint64_t)a * b; }
 #endif
 
+// Chains of 4 / 2 MADs in ONE asm statement: the hazard recognizer pads every inline-asm VALU
+// statement with an s_nop, so grouping cuts the pads 4x.  vv: both factors per-lane; vs: second
+// factor wave-uniform.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define NTT_MAD4(C1, C2)                                                                          \
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n\t"                                                   \
+      "v_mad_u64_u32 %0, %1, %4, %5, %0\n\t"                                                   \
+      "v_mad_u64_u32 %0, %1, %6, %7, %0\n\t"                                                   \
+      "v_mad_u64_u32 %0, %1, %8, %9, %0"                                                       \
+      : "+v"(acc), "=&s"(cc)                                                                    \
+      : "v"(a0), C2(b0), "v"(a1), C2(b1), "v"(a2), C2(b2), "v"(a3), C2(b3))
+#define NTT_MAD2(C2)                                                                              \
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n\t"                                                   \
+      "v_mad_u64_u32 %0, %1, %4, %5, %0"                                                       \
+      : "+v"(acc), "=&s"(cc)                                                                    \
+      : "v"(a0), C2(b0), "v"(a1), C2(b1))
+#define NTT_CV(x) "v"(x)
+#define NTT_CS(x) "s"(x)
+__device__ __forceinline__ uint64_t mad4vv(uint64_t acc, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1,
+                                           uint32_t a2, uint32_t b2, uint32_t a3, uint32_t b3) {
+  uint64_t cc;
+  NTT_MAD4(NTT_CV, NTT_CV);
+  return acc;
+}
+__device__ __forceinline__ uint64_t mad4vs(uint64_t acc, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1,
+                                           uint32_t a2, uint32_t b2, uint32_t a3, uint32_t b3) {
+  uint64_t cc;
+  NTT_MAD4(NTT_CV, NTT_CS);
+  return acc;
+}
+__device__ __forceinline__ uint64_t mad2vv(uint64_t acc, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1) {
+  uint64_t cc;
+  NTT_MAD2(NTT_CV);
+  return acc;
+}
+__device__ __forceinline__ uint64_t mad2vs(uint64_t acc, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1) {
+  uint64_t cc;
+  NTT_MAD2(NTT_CS);
+  return acc;
+}
+#undef NTT_MAD4
+#undef NTT_MAD2
+#undef NTT_CV
+#undef NTT_CS
+#else
+static inline uint64_t mad4vv(uint64_t acc, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1, uint32_t a2,
+                              uint32_t b2, uint32_t a3, uint32_t b3) {
+  return acc + (uint64_t)a0 * b0 + (uint64_t)a1 * b1 + (uint64_t)a2 * b2 + (uint64_t)a3 * b3;
+}
+static inline uint64_t mad4vs(uint64_t acc, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1, uint32_t a2,
+                              uint32_t b2, uint32_t a3, uint32_t b3) {
+  return mad4vv(acc, a0, b0, a1, b1, a2, b2, a3, b3);
+}
+static inline uint64_t mad2vv(uint64_t acc, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1) {
+  return acc + (uint64_t)a0 * b0 + (uint64_t)a1 * b1;
+}
+static inline uint64_t mad2vs(uint64_t acc, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1) {
+  return mad2vv(acc, a0, b0, a1, b1);
+}
+#endif
+
+// acc += sum_{i=lo}^{hi} a[i] * b[k - i] as one MAD chain, in asm groups of 4 / 2 / 1.
+// US: b is wave-uniform (SGPR operands).
+template <int L, bool US, int lo, int hi>
+F29_HD uint64_t mad_span(uint64_t acc, const uint32_t (&a)[L], const uint32_t (&b)[L], int k) {
+  if constexpr (hi - lo + 1 >= 4) {
+    acc = US ? mad4vs(acc, a[lo], b[k - lo], a[lo + 1], b[k - lo - 1], a[lo + 2], b[k - lo - 2], a[lo + 3],
+                      b[k - lo - 3])
+             : mad4vv(acc, a[lo], b[k - lo], a[lo + 1], b[k - lo - 1], a[lo + 2], b[k - lo - 2], a[lo + 3],
+                      b[k - lo - 3]);
+    return mad_span<L, US, lo + 4, hi>(acc, a, b, k);
+  } else if constexpr (hi - lo + 1 >= 2) {
+    acc = US ? mad2vs(acc, a[lo], b[k - lo], a[lo + 1], b[k - lo - 1])
+             : mad2vv(acc, a[lo], b[k - lo], a[lo + 1], b[k - lo - 1]);
+    return mad_span<L, US, lo + 2, hi>(acc, a, b, k);
+  } else if constexpr (hi - lo + 1 == 1) {
+    return US ? mad29s(a[lo], b[k - lo], acc) : mad29v(a[lo], b[k - lo], acc);
+  } else {
+    return acc;
+  }
+}
+
+// mulc29 with grouped asm MAD chains (same result as mulc29).
+template <int L, int K = L - 2>
+F29_HD void mulc29_hi(uint32_t (&q)[L], uint64_t& acc, const uint32_t (&x)[L], const uint32_t (&ws)[L]) {
+  if constexpr (K < 2 * L - 1) {
+    constexpr int lo = (K - (L - 1) > 0) ? K - (L - 1) : 0, hi = (K < L - 1) ? K : L - 1;
+    acc = mad_span<L, false, lo, hi>(acc, x, ws, K);
+    if constexpr (K >= L) q[K - L] = (uint32_t)acc & kMask29;
+    acc >>= 29;
+    mulc29_hi<L, K + 1>(q, acc, x, ws);
+  }
+}
+template <int L, int K = 0>
+F29_HD void mulc29_lo(uint32_t (&r)[L], uint64_t& acc, const uint32_t (&x)[L], const uint32_t (&w)[L],
+                      const uint32_t (&q)[L], const uint32_t (&pbar)[L]) {
+  if constexpr (K < L) {
+    acc = mad_span<L, false, 0, K>(acc, x, w, K);
+    acc = mad_span<L, true, 0, K>(acc, q, pbar, K);
+    r[K] = (uint32_t)acc & kMask29;
+    acc >>= 29;
+    mulc29_lo<L, K + 1>(r, acc, x, w, q, pbar);
+  }
+}
+template <int L>
+F29_HD void mulc29_blk(uint32_t (&r)[L], const uint32_t (&x)[L], const uint32_t (&w)[L], const uint32_t (&ws)[L],
+                       const uint32_t (&pbar)[L]) {
+  uint32_t q[L];
+  uint64_t acc = 0;
+  mulc29_hi<L>(q, acc, x, ws);
+  q[L - 1] = (uint32_t)acc;
+  acc = 0;
+  mulc29_lo<L>(r, acc, x, w, q, pbar);
+}
+
 // mont29 with every column accumulated in ONE dependent chain (same result as mont29).
 template <int L>
 F29_HD void mont29_chain(uint32_t (&r)[L], const uint32_t (&a)[L], const uint32_t (&b)[L], const Mod29<L>& M) {
@@ -189,6 +304,87 @@ F29_HD void mulc29(uint32_t (&r)[L], const uint32_t (&x)[L], const uint32_t (&w)
     for (int i = 0; i <= k; ++i) acc = mad29s(q[i], pbar[k - i], acc);
     r[k] = (uint32_t)acc & kMask29;
     acc >>= 29;
+  }
+}
+
+// mulc29 in plain C++ (the compiler schedules the MAD chains; no inline asm)
+template <int L>
+F29_HD void mulc29_cc(uint32_t (&r)[L], const uint32_t (&x)[L], const uint32_t (&w)[L], const uint32_t (&ws)[L],
+                   const uint32_t (&pbar)[L]) {
+  uint32_t q[L];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = L - 2; k < 2 * L - 1; ++k) {
+#pragma unroll
+    for (int i = (k - (L - 1) > 0 ? k - (L - 1) : 0); i <= (k < L - 1 ? k : L - 1); ++i)
+      acc += (uint64_t)x[i] * ws[k - i];
+    if (k >= L) q[k - L] = (uint32_t)acc & kMask29;
+    acc >>= 29;
+  }
+  q[L - 1] = (uint32_t)acc;
+  acc = 0;
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+#pragma unroll
+    for (int i = 0; i <= k; ++i) acc += (uint64_t)x[i] * w[k - i];
+#pragma unroll
+    for (int i = 0; i <= k; ++i) acc += (uint64_t)q[i] * pbar[k - i];
+    r[k] = (uint32_t)acc & kMask29;
+    acc >>= 29;
+  }
+}
+
+// r = a * b mod B (the low L limbs of the product), normalised.  45 MADs for L = 9.
+template <int L>
+F29_HD void mullo29(uint32_t (&r)[L], const uint32_t (&a)[L], const uint32_t (&b)[L]) {
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+#pragma unroll
+    for (int i = 0; i <= k; ++i) acc = mad29v(a[i], b[k - i], acc);
+    r[k] = (uint32_t)acc & kMask29;
+    acc >>= 29;
+  }
+}
+// r = (B - a) mod B for normalised a
+template <int L>
+F29_HD void neg29(uint32_t (&r)[L], const uint32_t (&a)[L]) {
+  uint32_t c = 1;
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    const uint32_t v = (kMask29 - a[i]) + c;
+    r[i] = v & kMask29;
+    c = v >> 29;
+  }
+}
+// Shoup companion of a canonical w: ws = floor(w * B / p), from wR = w * B mod p (canonical).
+// w * B = ws * p + wR exactly, so ws = (w * B - wR) / p = (-wR) * p^-1 mod B (pinvB = p^-1 mod B).
+template <int L>
+F29_HD void shoup_ws29(uint32_t (&ws)[L], const uint32_t (&wR)[L], const uint32_t (&pinvB)[L]) {
+  uint32_t t[L];
+  neg29<L>(t, wR);
+  mullo29<L>(ws, t, pinvB);
+}
+// p^-1 mod B by Newton iteration (host side, plan creation)
+template <int L>
+F29_HD void inv_mod_B29(uint32_t (&inv)[L], const uint32_t (&p)[L]) {
+  uint32_t i0 = 1;
+  for (int k = 0; k < 5; ++k) i0 *= 2 - p[0] * i0;  // p^-1 mod 2^32
+#pragma unroll
+  for (int i = 0; i < L; ++i) inv[i] = 0;
+  inv[0] = i0 & kMask29;
+  for (int bits = 29; bits < 29 * L; bits *= 2) {  // inv <- inv * (2 - p * inv) mod B
+    uint32_t t[L], u[L];
+    mullo29<L>(t, p, inv);
+    neg29<L>(u, t);
+    uint32_t c = 2;  // u += 2
+    for (int i = 0; i < L; ++i) {
+      const uint32_t v = u[i] + c;
+      u[i] = v & kMask29;
+      c = v >> 29;
+    }
+    mullo29<L>(t, inv, u);
+    for (int i = 0; i < L; ++i) inv[i] = t[i];
   }
 }
 

@@ -62,37 +62,39 @@ __device__ __forceinline__ uint32_t natural_index(uint32_t pi) {
 }
 
 // In-register DFT of size Q in {2,4,8} over x[base + d], d < Q (DIF radix-2 network): output X_k
-// lands in slot base + brev(k).  Lazy bounds (engines.hpp): inputs < 2p, outputs < 2Q p.
+// lands in slot base + brev(k).  Lazy bounds (engines.hpp): inputs < IN p, stage s offsets by
+// IN 2^(s-1) p, outputs < IN Q p.
 template <class E, int Q, int base>
 __device__ __forceinline__ void dft_q(uint32_t (&x)[8][E::W], const typename E::Args& F) {
+  constexpr int K1 = E::IN, K2 = 2 * E::IN, K3 = 4 * E::IN;
   if constexpr (Q == 2) {
-    E::template bfly_l<2>(x[base], x[base + 1], F);
+    E::template bfly_l<K1>(x[base], x[base + 1], F);
   } else if constexpr (Q == 4) {
-    E::template bfly_l<2>(x[base], x[base + 2], F);
-    E::template bfly_w_l<2>(x[base + 1], x[base + 3], F.w8[1], F);
-    E::template bfly_l<4>(x[base], x[base + 1], F);
-    E::template bfly_l<4>(x[base + 2], x[base + 3], F);
+    E::template bfly_l<K1>(x[base], x[base + 2], F);
+    E::template bfly_w_l<K1>(x[base + 1], x[base + 3], F.w8[1], F);
+    E::template bfly_l<K2>(x[base], x[base + 1], F);
+    E::template bfly_l<K2>(x[base + 2], x[base + 3], F);
   } else {
     static_assert(Q == 8, "radix");
-    E::template bfly_l<2>(x[base], x[base + 4], F);
-    E::template bfly_w_l<2>(x[base + 1], x[base + 5], F.w8[0], F);
-    E::template bfly_w_l<2>(x[base + 2], x[base + 6], F.w8[1], F);
-    E::template bfly_w_l<2>(x[base + 3], x[base + 7], F.w8[2], F);
-    E::template bfly_l<4>(x[base], x[base + 2], F);
-    E::template bfly_w_l<4>(x[base + 1], x[base + 3], F.w8[1], F);
-    E::template bfly_l<4>(x[base + 4], x[base + 6], F);
-    E::template bfly_w_l<4>(x[base + 5], x[base + 7], F.w8[1], F);
-    E::template bfly_l<8>(x[base], x[base + 1], F);
-    E::template bfly_l<8>(x[base + 2], x[base + 3], F);
-    E::template bfly_l<8>(x[base + 4], x[base + 5], F);
-    E::template bfly_l<8>(x[base + 6], x[base + 7], F);
+    E::template bfly_l<K1>(x[base], x[base + 4], F);
+    E::template bfly_w_l<K1>(x[base + 1], x[base + 5], F.w8[0], F);
+    E::template bfly_w_l<K1>(x[base + 2], x[base + 6], F.w8[1], F);
+    E::template bfly_w_l<K1>(x[base + 3], x[base + 7], F.w8[2], F);
+    E::template bfly_l<K2>(x[base], x[base + 2], F);
+    E::template bfly_w_l<K2>(x[base + 1], x[base + 3], F.w8[1], F);
+    E::template bfly_l<K2>(x[base + 4], x[base + 6], F);
+    E::template bfly_w_l<K2>(x[base + 5], x[base + 7], F.w8[1], F);
+    E::template bfly_l<K3>(x[base], x[base + 1], F);
+    E::template bfly_l<K3>(x[base + 2], x[base + 3], F);
+    E::template bfly_l<K3>(x[base + 4], x[base + 5], F);
+    E::template bfly_l<K3>(x[base + 6], x[base + 7], F);
   }
 }
 
 template <class E>
 __device__ __forceinline__ void twiddle_mul(uint32_t (&x)[E::W], const uint32_t* tab, uint32_t e,
                                             const typename E::Args& F) {
-  uint32_t w[E::W];
+  typename E::Tw w;
   E::tload(w, tab, e);
   E::mul(x, w, F);
 }
@@ -111,37 +113,45 @@ __device__ __forceinline__ void substage(uint32_t (&x)[8][E::W], uint32_t (&cl)[
                                          const PassArgs<E>& A, int t) {
   using S = Sched<LOGR>;
   constexpr int pqb = S::qb(s - 1), PQ = 1 << pqb, PG = 8 / PQ, psb = S::logsig(s - 1), plN = S::logN(s - 1);
-  if constexpr (s > 1) __syncthreads();  // everyone finished reading the previous exchange
-  static_for<PG>([&](auto J) {
-    constexpr int j = J;
-    const uint32_t g = pil[j];
-    const uint32_t rho = g >> psb, cp = g & ((1u << psb) - 1);
-    static_for<PQ>([&](auto K) {
-      constexpr int k = K;
-      const uint32_t pi = (rho << plN) + cp + (k << psb);
-      lds_put<E::LDSW, TE>(lds, lds_slot<T>(cl[j], pi), x[j * PQ + brev_bits(k, pqb)]);
+  constexpr int qb = S::qb(s), Q = 1 << qb, G = 8 / Q, sb = S::logsig(s), lN = S::logN(s);
+  using P = LdsParts<E::LDSW, E::LDS_SPLIT>;
+  static_for<P::PARTS>([&](auto PT) {
+    constexpr int part = PT;
+    if constexpr (s > 1 || part > 0) __syncthreads();  // everyone finished reading the previous round
+    static_for<PG>([&](auto J) {
+      constexpr int j = J;
+      const uint32_t g = pil[j];
+      const uint32_t rho = g >> psb, cp = g & ((1u << psb) - 1);
+      static_for<PQ>([&](auto K) {
+        constexpr int k = K;
+        const uint32_t pi = (rho << plN) + cp + (k << psb);
+        lds_put_part<E::LDSW, E::LDS_SPLIT, TE, part>(lds, lds_slot<T>(cl[j], pi), x[j * PQ + brev_bits(k, pqb)]);
+      });
+    });
+    __syncthreads();
+    static_for<G>([&](auto J) {
+      constexpr int j = J;
+      const uint32_t lam = t + NT * j;
+      const uint32_t c = lam % T, g = lam / T;
+      const uint32_t rho = g >> sb, cp = g & ((1u << sb) - 1);
+      static_for<Q>([&](auto D) {
+        constexpr int d = D;
+        const uint32_t pi = (rho << lN) + cp + (d << sb);
+        lds_get_part<E::LDSW, E::LDS_SPLIT, TE, part>(x[j * Q + d], lds, lds_slot<T>(c, pi));
+      });
     });
   });
-  __syncthreads();
-  constexpr int qb = S::qb(s), Q = 1 << qb, G = 8 / Q, sb = S::logsig(s), lN = S::logN(s);
   static_for<G>([&](auto J) {
     constexpr int j = J;
     const uint32_t lam = t + NT * j;
-    const uint32_t c = lam % T, g = lam / T;
-    const uint32_t rho = g >> sb, cp = g & ((1u << sb) - 1);
-    cl[j] = c;
-    pil[j] = g;
-    static_for<Q>([&](auto D) {
-      constexpr int d = D;
-      const uint32_t pi = (rho << lN) + cp + (d << sb);
-      lds_get<E::LDSW, TE>(x[j * Q + d], lds, lds_slot<T>(c, pi));
-    });
+    cl[j] = lam % T;
+    pil[j] = lam / T;
   });
   static_for<G>([&](auto J) {
     constexpr int j = J;
     dft_q<E, Q, j * Q>(x, A.F);
     if constexpr (s + 1 < S::nsub) {
-      E::template reduce_to_2p<2 * Q>(x[j * Q], A.F);  // k = 0: the only output not multiplied
+      E::template reduce<E::IN * Q, E::IN>(x[j * Q], A.F);  // k = 0: the only output not multiplied
       const uint32_t cp = pil[j] & ((1u << sb) - 1);
       static_for<Q - 1>([&](auto K1) {
         constexpr int k = K1 + 1;
@@ -152,14 +162,15 @@ __device__ __forceinline__ void substage(uint32_t (&x)[8][E::W], uint32_t (&cl)[
 }
 
 template <class E, int LOGR, int KIND, bool FULLTW>
-__global__ __launch_bounds__(256) void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
+void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                               const PassArgs<E> A) {
   using S = Sched<LOGR>;
   constexpr int TE = (KIND == KIND_SINGLE) ? (1 << LOGR) : tile_elems_w(E::LDSW);
   constexpr int T = TE >> LOGR;  // columns (column pass) or blocks (final / single) per workgroup
   constexpr int NT = TE / 8;     // threads
   static_assert(LOGR >= 3 && T >= 1, "radix");
-  __shared__ __attribute__((aligned(16))) uint32_t lds[TE * E::LDSW];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[TE * LdsParts<E::LDSW, E::LDS_SPLIT>::max_words()];
 
   const int t = threadIdx.x;
   if (t >= NT) return;
@@ -230,7 +241,7 @@ __global__ __launch_bounds__(256) void k_pass(const uint32_t* __restrict__ src, 
       constexpr int j = J;
       dft_q<E, Q, j * Q>(x, A.F);
       if constexpr (S::nsub > 1) {
-        E::template reduce_to_2p<2 * Q>(x[j * Q], A.F);  // k = 0: the only output not multiplied
+        E::template reduce<E::IN * Q, E::IN>(x[j * Q], A.F);  // k = 0: the only output not multiplied
         static_for<Q - 1>([&](auto K1) {
           constexpr int k = K1 + 1;
           twiddle_mul<E>(x[j * Q + brev_bits(k, qb)], A.tw_int, pil[j] * k, A.F);
@@ -260,32 +271,37 @@ __global__ __launch_bounds__(256) void k_pass(const uint32_t* __restrict__ src, 
         const uint32_t kn = natural_index<LOGR>(pi);
         size_t pos;
         if constexpr (KIND == KIND_COLUMN) {
-          uint32_t tl[E::W];
           if constexpr (FULLTW) {
-            // outer twiddle w_{N_i}^{col * kn} from the per-pass table, indexed like the data
-            // within a block (HBM-streamed for pass 1, L2-resident for later passes)
-            E::load(tl, A.tw_full, (size_t)(col0 + c) + ((size_t)kn << log_s));
+            // outer twiddle w_{N_i}^{col * kn} R_e from the per-pass table (HBM element format,
+            // indexed like the data within a block: HBM-streamed for pass 1, L2-resident later);
+            // the Montgomery product removes R_e.  32 B per entry instead of a 80-B Shoup pair.
+            uint32_t tw[E::W];
+            E::load(tw, A.tw_full, (size_t)(col0 + c) + ((size_t)kn << log_s));
+            E::mulv(v, tw, A.F);
           } else {
-            // outer twiddle w_{N_i}^{col * kn} = w_n^{(col * kn) << log_m}, two-level table
+            // outer twiddle w_{N_i}^{col * kn} = w_n^{(col * kn) << log_m} from the two-level
+            // tables: t = (lo R_e) * hi, then the Montgomery product v * t / R_e = v * lo * hi
             const size_t e = ((size_t)(col0 + c) * kn) << A.log_m;
-            uint32_t th[E::W];
+            typename E::Tw tl, th;
             E::tload(tl, A.tw_lo, (uint32_t)(e & ((1u << A.lo_bits) - 1)));
             E::tload(th, A.tw_hi, (uint32_t)(e >> A.lo_bits));
-            E::mul(tl, th, A.F);
+            E::mul(tl.w, th, A.F);
+            E::mulv(v, tl.w, A.F);
           }
-          E::mul(v, tl, A.F);
           pos = colbase + c + ((size_t)kn << log_s);
+          E::template store<E::MUL_OUT>(dst, pos, v, A.F);
         } else if constexpr (KIND == KIND_FINAL) {
-          E::template reduce_to_2p<2 * Q>(v, A.F);
           pos = (size_t)(k10 + c) + ((size_t)midrev << A.r1) + ((size_t)kn << (A.log_n - LOGR));
+          E::template store<E::IN * Q>(dst, pos, v, A.F);
         } else {
-          if (A.flags & 1u)
-            E::mul(v, A.F.ninv, A.F);
-          else
-            E::template reduce_to_2p<2 * Q>(v, A.F);
           pos = kn;
+          if (A.flags & 1u) {
+            E::mul(v, A.F.ninv, A.F);
+            E::template store<E::MUL_OUT>(dst, pos, v, A.F);
+          } else {
+            E::template store<E::IN * Q>(dst, pos, v, A.F);
+          }
         }
-        E::store(dst, pos, v, A.F);
       });
     });
   }
@@ -300,7 +316,8 @@ __global__ void k_dft_naive(const uint32_t* __restrict__ src, uint32_t* __restri
   uint32_t acc[E::W];
   if (k < n) {
     // acc = x_0 * w^0 (Montgomery by w^0 = R brings it to the engine's residue form)
-    uint32_t v[E::W], w[E::W];
+    uint32_t v[E::W];
+    typename E::Tw w;
     E::load(acc, src + boff, 0);
     E::tload(w, A.tw_int, 0);
     E::mul(acc, w, A.F);
@@ -309,18 +326,18 @@ __global__ void k_dft_naive(const uint32_t* __restrict__ src, uint32_t* __restri
       E::load(v, src + boff, j);
       E::tload(w, A.tw_int, (j * k) & (n - 1));
       E::mul(v, w, A.F);
-      uint32_t z[E::W];
-      for (int i = 0; i < E::W; ++i) z[i] = v[i];
-      E::bfly(acc, z, A.F);  // acc <- acc + v (the difference is discarded)
+      E::template bfly_l<E::IN>(acc, v, A.F);  // acc <- acc + v (the difference is discarded)
+      E::template reduce<2 * E::IN, E::IN>(acc, A.F);
     }
     if (A.flags & 1u) E::mul(acc, A.F.ninv, A.F);
   }
   __syncthreads();  // every thread has read src before anyone writes dst (in-place use)
-  if (k < n) E::store(dst + boff, k, acc, A.F);
+  if (k < n) E::template store<E::IN>(dst + boff, k, acc, A.F);
 }
 
-// Per-pass outer-twiddle table: out[c + (k << log_s)] = w_n^((c*k) << log_m) (engine Montgomery
-// value, stored canonical in the HBM element format), built on the device from the two-level tables.
+// Per-pass outer-twiddle table: out[c + (k << log_s)] = w_n^((c*k) << log_m) R_e mod p (R_e the
+// engine's Montgomery radix), canonical in the HBM element format, built on the device from the
+// two-level tables (lo_s = lo R_e, so lo_s * hi = w R_e).
 template <class E>
 __global__ void k_build_tw(uint32_t* __restrict__ out, size_t count, uint32_t log_s, uint32_t log_m,
                            const uint32_t* __restrict__ lo, const uint32_t* __restrict__ hi, uint32_t lo_bits,
@@ -329,11 +346,11 @@ __global__ void k_build_tw(uint32_t* __restrict__ out, size_t count, uint32_t lo
   if (idx >= count) return;
   const size_t c = idx & ((1ull << log_s) - 1), k = idx >> log_s;
   const size_t e = (c * k) << log_m;
-  uint32_t a[E::W], b[E::W];
+  typename E::Tw a, b;
   E::tload(a, lo, (uint32_t)(e & ((1ull << lo_bits) - 1)));
   E::tload(b, hi, (uint32_t)(e >> lo_bits));
-  E::mul(a, b, F);
-  E::store(out, idx, a, F);
+  E::mul(a.w, b, F);
+  E::template store<E::MUL_OUT>(out, idx, a.w, F);
 }
 
 template <class E>
@@ -348,7 +365,8 @@ hipError_t launch_build_tw(uint32_t* out, size_t count, uint32_t log_s, uint32_t
 // Multi-GPU four-step, local steps.  twiddle_pack: src is [rows][row_len] (row-major);
 // element (a, b) is multiplied by w_n^((row0 + a) * b) and written to dst block b / bw (bw =
 // row_len / G) at a * bw + b % bw, i.e. dst = [G][rows][bw]: one contiguous chunk per peer for the
-// all-to-all.  Twiddles from the plan's two-level tables (w_n^e = lo[e & mask] * hi[e >> lo_bits]).
+// all-to-all.  Twiddles from the plan's two-level tables: lo_s holds lo * R_e (R_e the engine's
+// Montgomery radix), so t = lo_s[e & mask] * hi[e >> lo_bits] = w_n^e R_e and mulv(x, t) = x w_n^e.
 template <class E>
 __global__ void k_twiddle_pack(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t log_rows,
                                uint32_t log_len, uint32_t log_bw, uint64_t row0, uint32_t log_n,
@@ -358,14 +376,15 @@ __global__ void k_twiddle_pack(const uint32_t* __restrict__ src, uint32_t* __res
   if (i >= (1ull << (log_rows + log_len))) return;
   const uint64_t a = i >> log_len, b = i & ((1ull << log_len) - 1);
   const uint64_t e = ((row0 + a) * b) & ((1ull << log_n) - 1);
-  uint32_t x[E::W], w[E::W], h[E::W];
+  uint32_t x[E::W];
+  typename E::Tw w, h;
   E::load(x, src, i);
   E::tload(w, lo, (uint32_t)(e & ((1ull << lo_bits) - 1)));
   E::tload(h, hi, (uint32_t)(e >> lo_bits));
-  E::mul(w, h, F);
-  E::mul(x, w, F);
+  E::mul(w.w, h, F);
+  E::mulv(x, w.w, F);
   const size_t blk = b >> log_bw, off = b & ((1ull << log_bw) - 1);
-  E::store(dst, (blk << (log_rows + log_bw)) + (a << log_bw) + off, x, F);
+  E::template store<E::MUL_OUT>(dst, (blk << (log_rows + log_bw)) + (a << log_bw) + off, x, F);
 }
 
 // dst[c][r] = src[r][c] for a rows x cols matrix of MEMW-word elements (32x32 tiles through LDS).
@@ -481,13 +500,14 @@ __global__ void k_pointwise_mul(const uint32_t* __restrict__ a, const uint32_t* 
                                 size_t n, const typename E::Args F, const uint32_t* __restrict__ r2) {
   const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
-  uint32_t x[E::W], y[E::W], z[E::W];
+  uint32_t x[E::W], y[E::W];
+  typename E::Tw z;  // R_e mod p as a twiddle: mulv leaves x y / R_e
   E::load(x, a, j);
   E::load(y, b, j);
   E::tload(z, r2, 0);
-  E::mul(x, y, F);
+  E::mulv(x, y, F);
   E::mul(x, z, F);
-  E::store(c, j, x, F);
+  E::template store<E::MUL_OUT>(c, j, x, F);
 }
 
 // ---------------------------------------------------------------------------- launchers

@@ -130,56 +130,66 @@ struct EngHost;
 template <int L, int W32>
 struct EngHost<Eng29<L, W32>> {
   static constexpr int NH = W32;
+  static constexpr int TW = Eng29<L, W32>::TW;
   using EA = typename Eng29<L, W32>::Args;
   HostField<NH> const* H = nullptr;
-  Vec<NH> kR{};  // 2^(29L) mod p, canonical
+  Vec<NH> kR{};          // B = 2^(29L) mod p, canonical
+  uint32_t pinvB[L] = {};  // p^-1 mod B
   void init(const HostField<NH>& h) {
     H = &h;
     Vec<NH> x{};
     x[0] = 1;
     for (int k = 0; k < 29 * L; ++k) x = h.add(x, x);
     kR = x;
+    uint32_t pw[NH], pl[L];
+    for (int i = 0; i < NH; ++i) pw[i] = h.M.p[i];
+    pack29<L, NH>(pl, pw);
+    inv_mod_B29<L>(pinvB, pl);
   }
-  // canonical c -> c * 2^(29L) mod p as TW words
-  void encode(const Vec<NH>& c, uint32_t* out) const {
-    Vec<NH> m = H->mul(c, H->to_mont(kR));  // mont32(c, kR * R32) = c * kR
-    uint32_t w[NH], x[L];
-    for (int i = 0; i < NH; ++i) w[i] = m[i];
+  static void limbs(const Vec<NH>& c, uint32_t (&x)[L]) {
+    uint32_t w[NH];
+    for (int i = 0; i < NH; ++i) w[i] = c[i];
     pack29<L, NH>(x, w);
-    for (int i = 0; i < Eng29<L, W32>::TW; ++i) out[i] = i < L ? x[i] : 0u;
   }
+  Vec<NH> times_B(const Vec<NH>& c) const { return H->mul(c, H->to_mont(kR)); }  // c B mod p
+  // canonical c -> Shoup table entry (c, floor(c B / p)) as TW words
+  void encode(const Vec<NH>& c, uint32_t* out) const {
+    uint32_t w[L], wr[L], ws[L];
+    limbs(c, w);
+    limbs(times_B(c), wr);
+    shoup_ws29<L>(ws, wr, pinvB);
+    for (int i = 0; i < TW; ++i) out[i] = i < L ? w[i] : (i < 2 * L ? ws[i - L] : 0u);
+  }
+  // entry whose value is c R_e (R_e = B): the left factor of the two-level twiddle products
+  void encode_scaled(const Vec<NH>& c, uint32_t* out) const { encode(times_B(c), out); }
   bool check_modulus(const uint32_t* p) const {
-    // p < 2^(32*W32 - 1) so that 2p fits the HBM words and 16p < R = 2^(29L)
-    return (p[NH - 1] >> 31) == 0 && 29 * L >= 32 * NH - 1 + 4;
+    // p < 2^(32*W32 - 1) so that 2p fits the HBM words and 32p < B = 2^(29L)
+    return (p[NH - 1] >> 31) == 0 && 29 * L >= 32 * NH - 1 + 5;
   }
   void fill_args(EA& A, const uint32_t* p, const Vec<NH>* w8, const Vec<NH>& ninv) const {
-    uint32_t pw[NH], p2w[NH];
-    uint32_t c = 0;
-    for (int i = 0; i < NH; ++i) {
-      pw[i] = p[i];
-      const uint64_t s = (uint64_t)p[i] + p[i] + c;
-      p2w[i] = (uint32_t)s;
-      c = (uint32_t)(s >> 32);
-    }
+    uint32_t pw[NH];
+    for (int i = 0; i < NH; ++i) pw[i] = p[i];
     pack29<L, NH>(A.M.p, pw);
-    pack29<L, NH>(A.M.p2, p2w);
-    // 4p, 8p: shift the normalised 2p limbs left and renormalise (values < 2^(29L))
-    for (int i = 0; i < L; ++i) {
-      A.p4[i] = A.M.p2[i] << 1;
-      A.p8[i] = A.M.p2[i] << 2;
+    for (int i = 0; i < L; ++i) A.kp[0][i] = A.M.p[i];
+    for (int j = 1; j < 5; ++j) {  // 2^j p: double the normalised limbs and renormalise
+      for (int i = 0; i < L; ++i) A.kp[j][i] = A.kp[j - 1][i] << 1;
+      norm_u<L>(A.kp[j]);
     }
-    norm_u<L>(A.p4);
-    norm_u<L>(A.p8);
+    for (int i = 0; i < L; ++i) A.M.p2[i] = A.kp[1][i];
+    neg29<L>(A.pbar, A.M.p);
     uint32_t inv = 1;
     for (int i = 0; i < 5; ++i) inv *= 2 - p[0] * inv;
     A.M.pinv = (0u - inv) & kMask29;
-    uint32_t tmp[Eng29<L, W32>::TW];
-    for (int k = 0; k < 3; ++k) {
-      encode(w8[k], tmp);
-      for (int i = 0; i < L; ++i) A.w8[k][i] = tmp[i];
-    }
-    encode(ninv, tmp);
-    for (int i = 0; i < L; ++i) A.ninv[i] = tmp[i];
+    uint32_t tmp[TW];
+    auto to_tw = [&](const Vec<NH>& c, typename Eng29<L, W32>::Tw& t) {
+      encode(c, tmp);
+      for (int i = 0; i < L; ++i) {
+        t.w[i] = tmp[i];
+        t.ws[i] = tmp[L + i];
+      }
+    };
+    for (int k = 0; k < 3; ++k) to_tw(w8[k], A.w8[k]);
+    to_tw(ninv, A.ninv);
   }
 };
 
@@ -193,11 +203,13 @@ struct EngHost<Eng32<N, MEMW_>> {
     const Vec<NH> m = H->to_mont(c);
     for (int i = 0; i < N; ++i) out[i] = m[i];
   }
+  // Montgomery form c R is already the R_e-scaled value
+  void encode_scaled(const Vec<NH>& c, uint32_t* out) const { encode(c, out); }
   bool check_modulus(const uint32_t* p) const { return p[NH - 1] < 0x7fffffffu; }
   void fill_args(EA& A, const uint32_t* p, const Vec<NH>* w8, const Vec<NH>& ninv) const {
     A.M = H->M;
-    for (int k = 0; k < 3; ++k) encode(w8[k], A.w8[k]);
-    encode(ninv, A.ninv);
+    for (int k = 0; k < 3; ++k) encode(w8[k], A.w8[k].w);
+    encode(ninv, A.ninv.w);
   }
 };
 
@@ -211,13 +223,14 @@ struct PlanImpl final : PlanBase {
   typename E::Args Ff{}, Fi{};
   uint32_t* d_tab = nullptr;
   uint32_t* d_scratch = nullptr;
-  uint32_t* d_full = nullptr;  // per-pass outer twiddle tables (HBM element format), both directions
+  uint32_t* d_full = nullptr;  // per-pass outer twiddle tables (w R_e, HBM element format), both directions
   size_t full_off[2][8] = {};  // element offsets into d_full, [dir][pass]
   bool use_full = false;
   size_t scratch_elems = 0;
   // table word offsets
   size_t off_int_f[8] = {0}, off_int_i[8] = {0};
   size_t off_lo_f = 0, off_hi_f = 0, off_lo_i = 0, off_hi_i = 0, off_hi_is = 0, off_r2 = 0;
+  size_t off_los_f = 0, off_los_i = 0;  // lo tables scaled by R_e (left factor of on-the-fly twiddles)
   unsigned lo_bits = 0;
   uint32_t nrand = 1, top_bits = 28;
 
@@ -329,12 +342,16 @@ struct PlanImpl final : PlanBase {
     schedule(log_n, tile_log_w(E::LDSW), r, npass);
     const bool twiddle_only = (flags & NTT_PLAN_TWIDDLE_ONLY) != 0;
     std::vector<uint32_t> host;
-    auto push_powers = [&](const Vec<NH>& base_m, uint64_t count, const Vec<NH>* scale_m) -> size_t {
+    auto push_powers = [&](const Vec<NH>& base_m, uint64_t count, const Vec<NH>* scale_m,
+                           bool scaled = false) -> size_t {
       const size_t off = host.size();
       Vec<NH> cur = scale_m ? *scale_m : H.r1;
       uint32_t enc[TW];
       for (uint64_t k = 0; k < count; ++k) {
-        EH.encode(H.from_mont(cur), enc);
+        if (scaled)
+          EH.encode_scaled(H.from_mont(cur), enc);
+        else
+          EH.encode(H.from_mont(cur), enc);
         host.insert(host.end(), enc, enc + TW);
         cur = H.mul(cur, base_m);
       }
@@ -355,13 +372,16 @@ struct PlanImpl final : PlanBase {
       {  // two-level tables of w_n^e (outer twiddles, four-step twiddle_pack)
         lo_bits = (log_n + 1) / 2;
         const size_t lo = push_powers(wn, 1ull << lo_bits, nullptr);
+        const size_t los = push_powers(wn, 1ull << lo_bits, nullptr, true);
         const Vec<NH> step = H.pow_u64(wn, 1ull << lo_bits);
         const size_t hi = push_powers(step, 1ull << (log_n - lo_bits), nullptr);
         if (dir == 0) {
           off_lo_f = lo;
+          off_los_f = los;
           off_hi_f = hi;
         } else {
           off_lo_i = lo;
+          off_los_i = los;
           off_hi_i = hi;
           off_hi_is = push_powers(step, 1ull << (log_n - lo_bits), &ninv_m);
         }
@@ -406,7 +426,7 @@ struct PlanImpl final : PlanBase {
       blk = log_n;
       for (unsigned i = 0; i + 1 < npass; ++i) {
         full_off[dir][i] = dir * elems + full_off[0][i];
-        const uint32_t* lo = d_tab + (dir ? off_lo_i : off_lo_f);
+        const uint32_t* lo = d_tab + (dir ? off_los_i : off_los_f);
         const uint32_t* hi = d_tab + (dir ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
         if (launch_build_tw<E>(d_full + full_off[dir][i] * MEMW, 1ull << blk, blk - r[i], log_n - blk, lo, hi,
                                lo_bits, dir ? Fi : Ff, nullptr) != hipSuccess)
@@ -475,7 +495,7 @@ struct PlanImpl final : PlanBase {
       for (unsigned i = 0; i + 1 < npass && e == hipSuccess; ++i) {
         PassArgs<E> A = base_args(inverse);
         A.tw_int = d_tab + off_int[i];
-        A.tw_lo = d_tab + (inverse ? off_lo_i : off_lo_f);
+        A.tw_lo = d_tab + (inverse ? off_los_i : off_los_f);
         A.tw_hi = d_tab + (inverse ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
         A.tw_full = use_full ? d_full + full_off[inverse ? 1 : 0][i] * MEMW : nullptr;
         A.log_blk = blk;
@@ -523,7 +543,7 @@ struct PlanImpl final : PlanBase {
   int twiddle_pack(const void* src, void* dst, unsigned log_rows, unsigned log_len, unsigned log_bw, uint64_t row0,
                    bool inverse, hipStream_t st) override {
     if (!src || !dst || src == dst || log_bw > log_len || log_rows + log_len > 40) return NTT_ERR_ARG;
-    const uint32_t* lo = d_tab + (inverse ? off_lo_i : off_lo_f);
+    const uint32_t* lo = d_tab + (inverse ? off_los_i : off_los_f);
     const uint32_t* hi = d_tab + (inverse ? off_hi_i : off_hi_f);
     hipError_t e = launch_twiddle_pack<E>(static_cast<const uint32_t*>(src), static_cast<uint32_t*>(dst), log_rows,
                                           log_len, log_bw, row0, log_n, lo, hi, lo_bits, inverse ? Fi : Ff, st);

@@ -11,7 +11,7 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libntt.so")
+LIB_PATH = os.environ.get("NTT_LIB_PATH") or os.path.join(HERE, "libntt.so")
 
 NTT_OK = 0
 NTT_FIELD_P469762049 = 0

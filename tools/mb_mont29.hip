@@ -21,13 +21,15 @@ using namespace ntt;
 constexpr int L = 9;
 constexpr int ITERS = 64;
 
-template <int ILP>
-__global__ __launch_bounds__(256) void k_mont(uint64_t* out, Mod29<L> M, uint32_t seed) {
+// VAR 0: mont29 (compiler-scheduled), 1: mont29_chain (asm single chain), 2: mulc29 (Shoup, asm)
+template <int ILP, int VAR>
+__global__ __launch_bounds__(256) void k_mont(uint64_t* out, Mod29<L> M, Mod29<L> S, uint32_t seed) {
   extern __shared__ uint32_t pad[];  // occupancy control only
-  uint32_t x[ILP][L], w[L];
+  uint32_t x[ILP][L], w[L], ws[L];
 #pragma unroll
   for (int i = 0; i < L; ++i) {
-    w[i] = (i * 0x9e3779b9u + seed) & 0x0fffffffu;
+    w[i] = (i * 0x9e3779b9u + seed + threadIdx.x) & 0x0fffffffu;
+    ws[i] = (i * 0x85ebca6bu + seed + threadIdx.x) & 0x1fffffffu;
 #pragma unroll
     for (int k = 0; k < ILP; ++k) x[k][i] = (threadIdx.x * 2654435761u + i * 40503u + k * 7u) & 0x0fffffffu;
   }
@@ -35,7 +37,11 @@ __global__ __launch_bounds__(256) void k_mont(uint64_t* out, Mod29<L> M, uint32_
 #pragma unroll
     for (int k = 0; k < ILP; ++k) {
       uint32_t r[L];
-      mont29<L>(r, x[k], w, M);
+      if constexpr (VAR == 0) mont29<L>(r, x[k], w, M);
+      else if constexpr (VAR == 1) mont29_chain<L>(r, x[k], w, M);
+      else if constexpr (VAR == 2) mulc29<L>(r, x[k], w, ws, S.p);
+      else if constexpr (VAR == 3) mulc29_cc<L>(r, x[k], w, ws, S.p);
+      else mulc29_blk<L>(r, x[k], w, ws, S.p);
 #pragma unroll
       for (int i = 0; i < L; ++i) x[k][i] = r[i];
     }
@@ -99,18 +105,18 @@ static int run_op(const char* name, void (*f)(uint64_t*, uint32_t), uint64_t* d)
   return 0;
 }
 
-template <int ILP>
-static int run(Mod29<L> M, uint64_t* d, int wg_per_cu) {
+template <int ILP, int VAR>
+static int run(Mod29<L> M, Mod29<L> S, uint64_t* d, int wg_per_cu) {
   const int threads = 256, blocks = 256 * wg_per_cu * 4;  // 4 rounds of full-chip residency
   const size_t lds = (160 * 1024) / wg_per_cu - 1024;
-  CHECK(hipFuncSetAttribute((const void*)k_mont<ILP>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(k_mont<ILP>, dim3(blocks), dim3(threads), lds, 0, d, M, 1u);
+  CHECK(hipFuncSetAttribute((const void*)(k_mont<ILP, VAR>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL((k_mont<ILP, VAR>), dim3(blocks), dim3(threads), lds, 0, d, M, S, 1u);
   CHECK(hipDeviceSynchronize());
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   CHECK(hipEventRecord(e0));
-  for (int r = 0; r < 3; ++r) hipLaunchKernelGGL(k_mont<ILP>, dim3(blocks), dim3(threads), lds, 0, d, M, 1u);
+  for (int r = 0; r < 3; ++r) hipLaunchKernelGGL((k_mont<ILP, VAR>), dim3(blocks), dim3(threads), lds, 0, d, M, S, 1u);
   CHECK(hipEventRecord(e1));
   CHECK(hipEventSynchronize(e1));
   float ms;
@@ -118,8 +124,9 @@ static int run(Mod29<L> M, uint64_t* d, int wg_per_cu) {
   const double muls = 3.0 * blocks * threads * (double)ITERS * ILP;
   const double rate = muls / (ms * 1e-3);
   const double cyc = 1024.0 * 2.4e9 / (rate / 64.0);  // SIMD cycles per wave-level product @2.4 GHz
-  printf("{\"ilp\": %d, \"waves_per_simd\": %d, \"Gmul_per_s\": %.2f, \"simd_cycles_per_wave_mul\": %.1f}\n", ILP,
-         wg_per_cu, rate / 1e9, cyc);
+  static const char* names[] = {"mont29", "mont29_chain", "mulc29_shoup", "mulc29_shoup_cc", "mulc29_shoup_blk"};
+  printf("{\"variant\": \"%s\", \"ilp\": %d, \"waves_per_simd\": %d, \"Gmul_per_s\": %.2f, "
+         "\"simd_cycles_per_wave_mul\": %.1f}\n", names[VAR], ILP, wg_per_cu, rate / 1e9, cyc);
   return 0;
 }
 
@@ -138,10 +145,20 @@ int main() {
       run_op("v_add3_u32", k_add3, d) || run_op("v_bfe_u32", k_bfe, d) || run_op("v_and_or_b32", k_andor, d) ||
       run_op("v_lshl_or_b32", k_lshlor, d) || run_op("v_mad_u32_u24", k_mad24, d) || run_op("v_ashrrev_i32", k_ashr, d))
     return 1;
-  for (int occ : {1, 2, 3, 4, 8}) {
-    if (run<1>(M, d, occ)) return 1;
-    if (run<2>(M, d, occ)) return 1;
-    if (run<4>(M, d, occ)) return 1;
+  Mod29<L> S{};  // S.p = pbar = 2^(29L) - p
+  {
+    uint32_t borrow = 1;
+    for (int i = 0; i < L; ++i) {
+      uint32_t v = (kMask29 - M.p[i]) + borrow;
+      S.p[i] = v & kMask29;
+      borrow = v >> 29;
+    }
+  }
+  for (int occ : {2, 3}) {
+    if (run<1, 0>(M, S, d, occ) || run<2, 0>(M, S, d, occ)) return 1;
+    if (run<1, 2>(M, S, d, occ) || run<2, 2>(M, S, d, occ)) return 1;
+    if (run<1, 3>(M, S, d, occ) || run<2, 3>(M, S, d, occ)) return 1;
+    if (run<1, 4>(M, S, d, occ) || run<2, 4>(M, S, d, occ)) return 1;
   }
   return 0;
 }
