@@ -38,6 +38,8 @@ struct Eng29 {
   // exchanges) spills ~300 B/thread with the Shoup operands live and measured 15 % slower.
   static constexpr int WAVES_PER_EU = (L <= 9) ? NTT_WAVES_256 : 2;
   static constexpr bool LDS_SPLIT = WAVES_PER_EU >= 3;
+  // quotient-estimate reduction needs p's top limb >= 2^18: possible only when 29L - 18 <= 255
+  static constexpr bool FASTRED = 29 * L - 18 <= 255;
   struct Tw {
     uint32_t w[L];   // canonical twiddle
     uint32_t ws[L];  // floor(w * B / p)
@@ -48,6 +50,8 @@ struct Eng29 {
     uint32_t pbar[L];     // B - p (Shoup)
     Tw w8[3];             // w_8^1, w_8^2, w_8^3
     Tw ninv;              // n^-1
+    float red_inv;        // 1 / (p_top + 1) rounded down (quotient-estimate reduction)
+    uint32_t red_ok;      // p_top >= 2^18: the top-limb quotient estimate is within 1
   };
 
   __device__ static __forceinline__ void load(uint32_t (&x)[W], const uint32_t* __restrict__ base, size_t idx) {
@@ -62,19 +66,54 @@ struct Eng29 {
   }
   // x < FROM p (power of two) -> x < TO p by conditional subtractions of FROM/2 p, ..., TO p
   template <int FROM, int TO>
-  __device__ static __forceinline__ void reduce(uint32_t (&x)[W], const Args& A) {
+  __device__ static __forceinline__ void reduce_chain(uint32_t (&x)[W], const Args& A) {
     static_assert(FROM <= 32 && TO >= 1, "lazy bound");
     if constexpr (FROM > TO) {
       constexpr int j = __builtin_ctz(FROM / 2);
       cond_sub<L>(x, A.kp[j]);
-      reduce<FROM / 2, TO>(x, A);
+      reduce_chain<FROM / 2, TO>(x, A);
     }
   }
+  // x < 64p -> [0, 2p): x - q p with q = floor(x_top / (p_top + 1)) (float estimate biased low by
+  // 2^-10), which is floor(x / p) or one less when p_top >= 2^18.  x - q p = (x + q pbar) mod B.
+  // 9 MADs + ~30 simple ops instead of up to four conditional subtractions.
+  __device__ static __forceinline__ void reduce_top(uint32_t (&x)[W], const Args& A) {
+    const float qf = __builtin_fmaf((float)x[L - 1], A.red_inv, -0x1p-10f);
+    const uint32_t q = qf > 0.f ? (uint32_t)qf : 0u;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      acc = (acc >> 29) + x[i] + (uint64_t)q * A.pbar[i];
+      x[i] = (uint32_t)acc & kMask29;
+    }
+  }
+  // FAST (a kernel template flag, chosen per plan from Args::red_ok): quotient-estimate reduction
+  // for the large drops.  A runtime branch here makes the compiler sink the two paths' kp[] uses into
+  // one dynamically indexed access and copy the kernel arguments to scratch, hence the template.
+  template <int FROM, int TO, bool FAST = false>
+  __device__ static __forceinline__ void reduce(uint32_t (&x)[W], const Args& A) {
+    if constexpr (FAST && FROM > 4 && TO <= 4) {
+      reduce_top(x, A);
+      if constexpr (TO == 1) cond_sub<L>(x, A.kp[0]);
+    } else {
+      reduce_chain<FROM, TO>(x, A);
+    }
+  }
+  // x < BOUND p -> x < 2p (fits the HBM words: p < 2^255) -> HBM.  Between passes only.
+  template <int BOUND, bool FAST = false>
+  __device__ static __forceinline__ void store_lazy(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
+                                                    const Args& A) {
+    reduce<BOUND, 2, FAST>(x, A);
+    put(base, idx, x);
+  }
   // x < BOUND p -> canonical -> HBM
-  template <int BOUND>
+  template <int BOUND, bool FAST = false>
   __device__ static __forceinline__ void store(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
                                                const Args& A) {
-    reduce<BOUND, 1>(x, A);
+    reduce<BOUND, 1, FAST>(x, A);
+    put(base, idx, x);
+  }
+  __device__ static __forceinline__ void put(uint32_t* __restrict__ base, size_t idx, const uint32_t (&x)[W]) {
     uint32_t w[W32];
     unpack29<L, W32>(w, x);
     uint4* p = reinterpret_cast<uint4*>(base + idx * W32);
@@ -173,9 +212,15 @@ struct Eng32 {
       }
     }
   }
-  template <int FROM, int TO>
+  static constexpr bool FASTRED = false;
+  template <int FROM, int TO, bool FAST = false>
   __device__ static __forceinline__ void reduce(uint32_t (&)[W], const Args&) {}
-  template <int BOUND>
+  template <int BOUND, bool FAST = false>
+  __device__ static __forceinline__ void store_lazy(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
+                                                    const Args& A) {
+    store<BOUND>(base, idx, x, A);
+  }
+  template <int BOUND, bool FAST = false>
   __device__ static __forceinline__ void store(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
                                                const Args&) {
     if constexpr (N == 1) {

@@ -108,7 +108,7 @@ __device__ __forceinline__ uint32_t lds_slot(uint32_t c, uint32_t pi) {
 }
 
 // One LDS exchange + in-register radix-Q sub-stage s (s >= 1).
-template <class E, int LOGR, int T, int TE, int NT, int s>
+template <class E, int LOGR, int T, int TE, int NT, int s, bool FAST>
 __device__ __forceinline__ void substage(uint32_t (&x)[8][E::W], uint32_t (&cl)[4], uint32_t (&pil)[4], uint32_t* lds,
                                          const PassArgs<E>& A, int t) {
   using S = Sched<LOGR>;
@@ -151,7 +151,7 @@ __device__ __forceinline__ void substage(uint32_t (&x)[8][E::W], uint32_t (&cl)[
     constexpr int j = J;
     dft_q<E, Q, j * Q>(x, A.F);
     if constexpr (s + 1 < S::nsub) {
-      E::template reduce<E::IN * Q, E::IN>(x[j * Q], A.F);  // k = 0: the only output not multiplied
+      E::template reduce<E::IN * Q, E::IN, FAST>(x[j * Q], A.F);  // k = 0: the only output not multiplied
       const uint32_t cp = pil[j] & ((1u << sb) - 1);
       static_for<Q - 1>([&](auto K1) {
         constexpr int k = K1 + 1;
@@ -161,7 +161,7 @@ __device__ __forceinline__ void substage(uint32_t (&x)[8][E::W], uint32_t (&cl)[
   });
 }
 
-template <class E, int LOGR, int KIND, bool FULLTW>
+template <class E, int LOGR, int KIND, bool FULLTW, bool FAST>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
 void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                               const PassArgs<E> A) {
@@ -241,7 +241,7 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
       constexpr int j = J;
       dft_q<E, Q, j * Q>(x, A.F);
       if constexpr (S::nsub > 1) {
-        E::template reduce<E::IN * Q, E::IN>(x[j * Q], A.F);  // k = 0: the only output not multiplied
+        E::template reduce<E::IN * Q, E::IN, FAST>(x[j * Q], A.F);  // k = 0: the only output not multiplied
         static_for<Q - 1>([&](auto K1) {
           constexpr int k = K1 + 1;
           twiddle_mul<E>(x[j * Q + brev_bits(k, qb)], A.tw_int, pil[j] * k, A.F);
@@ -251,9 +251,9 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
   }
 
   // ------------------------------------------------------------------ sub-stages 1..nsub-1 via LDS
-  if constexpr (S::nsub > 1) substage<E, LOGR, T, TE, NT, 1>(x, cl, pil, lds, A, t);
-  if constexpr (S::nsub > 2) substage<E, LOGR, T, TE, NT, 2>(x, cl, pil, lds, A, t);
-  if constexpr (S::nsub > 3) substage<E, LOGR, T, TE, NT, 3>(x, cl, pil, lds, A, t);
+  if constexpr (S::nsub > 1) substage<E, LOGR, T, TE, NT, 1, FAST>(x, cl, pil, lds, A, t);
+  if constexpr (S::nsub > 2) substage<E, LOGR, T, TE, NT, 2, FAST>(x, cl, pil, lds, A, t);
+  if constexpr (S::nsub > 3) substage<E, LOGR, T, TE, NT, 3, FAST>(x, cl, pil, lds, A, t);
 
   // ------------------------------------------------------------------ output
   {
@@ -289,17 +289,17 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
             E::mulv(v, tl.w, A.F);
           }
           pos = colbase + c + ((size_t)kn << log_s);
-          E::template store<E::MUL_OUT>(dst, pos, v, A.F);
+          E::template store_lazy<E::MUL_OUT, FAST>(dst, pos, v, A.F);  // scratch: < 2p, read by the next pass
         } else if constexpr (KIND == KIND_FINAL) {
           pos = (size_t)(k10 + c) + ((size_t)midrev << A.r1) + ((size_t)kn << (A.log_n - LOGR));
-          E::template store<E::IN * Q>(dst, pos, v, A.F);
+          E::template store<E::IN * Q, FAST>(dst, pos, v, A.F);
         } else {
           pos = kn;
           if (A.flags & 1u) {
             E::mul(v, A.F.ninv, A.F);
-            E::template store<E::MUL_OUT>(dst, pos, v, A.F);
+            E::template store<E::MUL_OUT, FAST>(dst, pos, v, A.F);
           } else {
-            E::template store<E::IN * Q>(dst, pos, v, A.F);
+            E::template store<E::IN * Q, FAST>(dst, pos, v, A.F);
           }
         }
       });
@@ -524,13 +524,25 @@ static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassAr
     constexpr int TE = (KIND == KIND_SINGLE) ? (1 << LOGR) : (1 << TL);
     constexpr int NT = TE / 8;
     const dim3 g(grid, batch), b(NT < 64 ? 64 : NT);
-    if constexpr (KIND == KIND_COLUMN) {
-      if (A.tw_full) {
-        hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true>), g, b, 0, st, src, dst, A);
+    if constexpr (E::FASTRED) {
+      if (A.F.red_ok) {
+        if constexpr (KIND == KIND_COLUMN) {
+          if (A.tw_full) {
+            hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true, true>), g, b, 0, st, src, dst, A);
+            return hipGetLastError();
+          }
+        }
+        hipLaunchKernelGGL((k_pass<E, LOGR, KIND, false, true>), g, b, 0, st, src, dst, A);
         return hipGetLastError();
       }
     }
-    hipLaunchKernelGGL((k_pass<E, LOGR, KIND, false>), g, b, 0, st, src, dst, A);
+    if constexpr (KIND == KIND_COLUMN) {
+      if (A.tw_full) {
+        hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true, false>), g, b, 0, st, src, dst, A);
+        return hipGetLastError();
+      }
+    }
+    hipLaunchKernelGGL((k_pass<E, LOGR, KIND, false, false>), g, b, 0, st, src, dst, A);
     return hipGetLastError();
   }
 }

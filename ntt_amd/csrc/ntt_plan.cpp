@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -190,6 +191,9 @@ struct EngHost<Eng29<L, W32>> {
     };
     for (int k = 0; k < 3; ++k) to_tw(w8[k], A.w8[k]);
     to_tw(ninv, A.ninv);
+    const uint32_t ptop = A.M.p[L - 1];
+    A.red_ok = ptop >= (1u << 18) ? 1u : 0u;
+    A.red_inv = std::nextafter(1.0f / (float)(ptop + 1u), 0.0f);
   }
 };
 
