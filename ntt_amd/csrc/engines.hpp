@@ -52,7 +52,12 @@ struct Eng29 {
     Tw ninv;              // n^-1
     float red_inv;        // 1 / (p_top + 1) rounded down (quotient-estimate reduction)
     uint32_t red_ok;      // p_top >= 2^18: the top-limb quotient estimate is within 1
+    uint32_t pc[5][L];    // padded offsets K p for the unnormalised butterflies (PC_* below)
   };
+  // Padded offsets: value K p, limbs c_0 = kp_0 + P, c_i = kp_i + P - P/2^29 (0 < i < 8),
+  // c_8 = kp_8 - P/2^29, so that c_i >= P > b_i for limb bound P and a - b + C never goes negative
+  // limb-wise; K = (value bound of b) + 1 keeps the top limb non-negative when p_top >= 3.
+  enum : int { PC_5_29 = 0, PC_9_30 = 1, PC_4_29 = 2, PC_17_29 = 3, PC_7_30 = 4 };
 
   __device__ static __forceinline__ void load(uint32_t (&x)[W], const uint32_t* __restrict__ base, size_t idx) {
     uint32_t w[W32];
@@ -176,6 +181,23 @@ struct Eng29 {
     bfly_l<K>(a, b, A);
     mul(b, t, A);
   }
+  // ---- unnormalised butterflies (FAST engines; limb/value bounds tracked in dft_q_fast)
+  template <int CI>
+  __device__ static __forceinline__ void bfly_raw(uint32_t (&a)[W], uint32_t (&b)[W], const Args& A) {
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      const uint32_t x = a[i], y = b[i];
+      a[i] = x + y;
+      b[i] = x - y + A.pc[CI][i];
+    }
+  }
+  template <int CI>
+  __device__ static __forceinline__ void bfly_raw_w(uint32_t (&a)[W], uint32_t (&b)[W], const Tw& t,
+                                                    const Args& A) {
+    bfly_raw<CI>(a, b, A);
+    mul(b, t, A);
+  }
+  __device__ static __forceinline__ void norm(uint32_t (&x)[W]) { norm_u<L>(x); }
 };
 
 // ------------------------------------------------------------------------------ 32-bit engine

@@ -91,6 +91,52 @@ __device__ __forceinline__ void dft_q(uint32_t (&x)[8][E::W], const typename E::
   }
 }
 
+// The same DFTs with unnormalised butterflies (FAST Eng29 engines): limbs grow past 29 bits and are
+// carry-normalised only where a later stage could overflow 32 bits.  (limb bound, value bound / p)
+// per slot, inputs (2^29, 4):
+//   Q = 8  stage 1: s (2^30, 8), d (1.5 2^30, 9), d * w -> (2^29, 3)
+//          stage 2: x0,x1 (2^31, 16)  x2 (2.5 2^30, 17)  x4 (2^31, 12)  x5 (2^30, 6)  x6 (2.5 2^30, 13)
+//          normalise x0 x1 x2 x4 x6; stage 3 outputs <= (2^31, 33)
+//   Q = 4  stage 2 outputs <= (2.5 2^30, 17); Q = 2: (1.5 2^30, 9)
+// Products accept limbs < 2^31.6 (64-bit column sums) and values < B = 2^261 (33p < 2^260).
+template <class E, int Q, int base>
+__device__ __forceinline__ void dft_q_fast(uint32_t (&x)[8][E::W], const typename E::Args& F) {
+  if constexpr (Q == 2) {
+    E::template bfly_raw<E::PC_5_29>(x[base], x[base + 1], F);
+  } else if constexpr (Q == 4) {
+    E::template bfly_raw<E::PC_5_29>(x[base], x[base + 2], F);
+    E::template bfly_raw_w<E::PC_5_29>(x[base + 1], x[base + 3], F.w8[1], F);
+    E::template bfly_raw<E::PC_9_30>(x[base], x[base + 1], F);
+    E::template bfly_raw<E::PC_4_29>(x[base + 2], x[base + 3], F);
+  } else {
+    static_assert(Q == 8, "radix");
+    E::template bfly_raw<E::PC_5_29>(x[base], x[base + 4], F);
+    E::template bfly_raw_w<E::PC_5_29>(x[base + 1], x[base + 5], F.w8[0], F);
+    E::template bfly_raw_w<E::PC_5_29>(x[base + 2], x[base + 6], F.w8[1], F);
+    E::template bfly_raw_w<E::PC_5_29>(x[base + 3], x[base + 7], F.w8[2], F);
+    E::template bfly_raw<E::PC_9_30>(x[base], x[base + 2], F);
+    E::template bfly_raw_w<E::PC_9_30>(x[base + 1], x[base + 3], F.w8[1], F);
+    E::template bfly_raw<E::PC_4_29>(x[base + 4], x[base + 6], F);
+    E::template bfly_raw_w<E::PC_4_29>(x[base + 5], x[base + 7], F.w8[1], F);
+    E::norm(x[base]);
+    E::norm(x[base + 1]);
+    E::norm(x[base + 2]);
+    E::norm(x[base + 4]);
+    E::norm(x[base + 6]);
+    E::template bfly_raw<E::PC_17_29>(x[base], x[base + 1], F);
+    E::template bfly_raw<E::PC_4_29>(x[base + 2], x[base + 3], F);
+    E::template bfly_raw<E::PC_7_30>(x[base + 4], x[base + 5], F);
+    E::template bfly_raw<E::PC_4_29>(x[base + 6], x[base + 7], F);
+  }
+}
+template <class E, int Q, int base, bool FAST>
+__device__ __forceinline__ void dft(uint32_t (&x)[8][E::W], const typename E::Args& F) {
+  if constexpr (FAST)
+    dft_q_fast<E, Q, base>(x, F);
+  else
+    dft_q<E, Q, base>(x, F);
+}
+
 template <class E>
 __device__ __forceinline__ void twiddle_mul(uint32_t (&x)[E::W], const uint32_t* tab, uint32_t e,
                                             const typename E::Args& F) {
@@ -149,7 +195,7 @@ __device__ __forceinline__ void substage(uint32_t (&x)[8][E::W], uint32_t (&cl)[
   });
   static_for<G>([&](auto J) {
     constexpr int j = J;
-    dft_q<E, Q, j * Q>(x, A.F);
+    dft<E, Q, j * Q, FAST>(x, A.F);
     if constexpr (s + 1 < S::nsub) {
       E::template reduce<E::IN * Q, E::IN, FAST>(x[j * Q], A.F);  // k = 0: the only output not multiplied
       const uint32_t cp = pil[j] & ((1u << sb) - 1);
@@ -239,7 +285,7 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
     });
     static_for<G>([&](auto J) {
       constexpr int j = J;
-      dft_q<E, Q, j * Q>(x, A.F);
+      dft<E, Q, j * Q, FAST>(x, A.F);
       if constexpr (S::nsub > 1) {
         E::template reduce<E::IN * Q, E::IN, FAST>(x[j * Q], A.F);  // k = 0: the only output not multiplied
         static_for<Q - 1>([&](auto K1) {

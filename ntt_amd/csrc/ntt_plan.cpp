@@ -194,6 +194,27 @@ struct EngHost<Eng29<L, W32>> {
     const uint32_t ptop = A.M.p[L - 1];
     A.red_ok = ptop >= (1u << 18) ? 1u : 0u;
     A.red_inv = std::nextafter(1.0f / (float)(ptop + 1u), 0.0f);
+    // padded offsets for the unnormalised butterflies (used only when red_ok: p_top >= 3)
+    auto padded = [&](uint32_t K, uint32_t pad, uint32_t* c) {
+      uint32_t kp[L];
+      uint64_t carry = 0;
+      for (int i = 0; i < L; ++i) {
+        const uint64_t v = (uint64_t)A.M.p[i] * K + carry;
+        kp[i] = (uint32_t)v & kMask29;
+        carry = v >> 29;
+      }
+      kp[L - 1] += (uint32_t)(carry << 29);  // K p < 2^(29L): carry is 0 for the supported fields
+      const uint32_t b = pad >> 29;
+      c[0] = kp[0] + pad;
+      for (int i = 1; i + 1 < L; ++i) c[i] = kp[i] + pad - b;
+      c[L - 1] = kp[L - 1] - b;
+    };
+    using E29 = Eng29<L, W32>;
+    padded(5, 1u << 29, A.pc[E29::PC_5_29]);
+    padded(9, 1u << 30, A.pc[E29::PC_9_30]);
+    padded(4, 1u << 29, A.pc[E29::PC_4_29]);
+    padded(17, 1u << 29, A.pc[E29::PC_17_29]);
+    padded(7, 1u << 30, A.pc[E29::PC_7_30]);
   }
 };
 
