@@ -15,8 +15,9 @@ SplitMix64 limbs), resident in HBM when the timed region starts.
   (SURVEY §8e, strong scaling; e.g. BASELINE config 4: --four-step --log-n 28 on 8 GPUs).
 
 Rank 0 prints one JSON line with `roofline` (HBM roofline of the dominant kernel, measured with
-HIP events on its launch stream inside the timed region) and `cpu_baseline` (the C oracle on the
-host, a bounded sample).
+HIP events on its launch stream inside the timed region), `valu_roofline` (the same launch against
+the v_mad_u64_u32 issue peak: the kernels are bound by 256-bit multiply-adds, not by HBM; see
+DESIGN.md §7) and `cpu_baseline` (the C oracle on the host, a bounded sample).
 """
 from __future__ import annotations
 
@@ -32,6 +33,23 @@ sys.path.insert(0, HERE)
 
 METRIC = "field-elements/sec, 2^24 forward NTT over BN254 Fr; achieved HBM GB/s vs peak"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# v_mad_u64_u32 issue peak, 8 independent chains per wave, every SIMD busy (tools/mb_isa.hip,
+# profiles/r01_mb_isa.txt): 33.8e12 lane-MADs/s
+MAD_PEAK_T = 33.8
+SHOUP_MADS, MONT_MADS = 143, 162  # v_mad_u64_u32 per 256-bit product (field29.hpp)
+
+
+def pass_mads(log_r: int, column: bool) -> float:
+    """v_mad_u64_u32 per element in one pass of radix 2^log_r (ntt_kernels_impl.hpp): radix-8/4/2
+    sub-stages with 5/8, 1/4, 0 internal products per element, (Q-1)/Q twiddle products between
+    sub-stages (Shoup), and in column passes one outer-twiddle Montgomery product."""
+    subs, r = [], log_r
+    while r > 0:
+        subs.append(min(3, r))
+        r -= min(3, r)
+    internal = {3: 5 / 8, 2: 1 / 4, 1: 0.0}
+    shoup = sum(internal[q] for q in subs) + sum((2 ** q - 1) / 2 ** q for q in subs[:-1])
+    return shoup * SHOUP_MADS + (MONT_MADS if column else 0)
 FIELD_NAMES = {0: "P469762049", 1: "BN254_FR", 2: "BLS12_381_FR"}
 
 
@@ -88,6 +106,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # one rank per GPU; the modulo only matters when rehearsing several ranks on one device
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     n = 1 << args.log_n
 
@@ -97,7 +117,10 @@ def main():
         os.environ.setdefault("MASTER_PORT", "29512")
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if args.four_step:  # the data path exchanges over RCCL (all-to-all)
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:  # independent transforms: the only collectives are the timing barrier and max
+            dist.init_process_group("gloo")
     if args.four_step:
         from ntt_amd.distributed import DistNTT
         eng = DistNTT(field_id=args.field, log_n=args.log_n, limbs64=args.limbs, device=local)
@@ -137,7 +160,8 @@ def main():
 
     elapsed = t1 - t0
     if use_dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dev = f"cuda:{local}" if args.four_step else "cpu"
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms_per_step = elapsed / args.steps * 1e3
@@ -159,8 +183,9 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if args.four_step else "weak",
         "vs_baseline": None,
-        "dtype": "uint256 (8x32-bit limbs, Montgomery)" if args.limbs == 4 else
-                 ("uint384 (12x32-bit limbs, Montgomery)" if args.limbs == 6 else "uint32 Montgomery"),
+        "dtype": ("u256 mod p: 9 x 29-bit limbs, u32 x u32 + u64 MAD (v_mad_u64_u32)" if args.limbs == 4 else
+                  ("u384 mod p: 14 x 29-bit limbs, u32 x u32 + u64 MAD" if args.limbs == 6 else
+                   "u32 mod p (Montgomery)")),
         "data": "synthetic: SplitMix64 field elements (SURVEY §8d vector B, seed 2), resident in HBM",
         "config": {"workload": f"2^{args.log_n}-point {'inverse' if args.inverse else 'forward'} NTT, "
                                f"{FIELD_NAMES[args.field]}, {args.limbs}x64-bit limbs, natural order, in place",
@@ -178,7 +203,7 @@ def main():
         local_n = n // world if args.four_step else n
         alg_bytes = 2 * local_n * elem_bytes
         achieved = alg_bytes / (launch_avg[k] * 1e-3) / 1e9
-        tag = f"f{args.field}_L{args.limbs}_n{args.log_n}_w{world}"
+        tag = f"f{args.field}_L{args.limbs}_n{args.log_n}_w{world if args.four_step else 1}"
         traffic = load_traffic(tag)
         out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                            "frac": achieved / HBM_PEAK_GBPS,
@@ -188,6 +213,15 @@ def main():
                            "launch_ms": launch_avg}
         total_alg = 2 * local_n * elem_bytes * max(1, len(launch_avg))
         out["hbm_effective_gbps_per_gpu"] = total_alg / (ms_per_step * 1e-3) / 1e9
+        if args.limbs == 4 and args.field in (1, 2) and not args.four_step and len(passes) == len(launch_avg) \
+                and len(passes) >= 2:
+            # compute roofline of the same launch: MADs issued per launch / its duration vs the
+            # v_mad_u64_u32 issue peak (the binding resource)
+            mads = local_n * pass_mads(passes[k], column=k + 1 < len(passes))
+            ach = mads / (launch_avg[k] * 1e-3) / 1e12
+            out["valu_roofline"] = {"bound": "valu (v_mad_u64_u32 issue)", "achieved": ach, "peak": MAD_PEAK_T,
+                                    "unit": "T lane-MAD/s", "frac": ach / MAD_PEAK_T,
+                                    "mads_per_launch": mads, "kernel": f"launch {k} of {len(launch_avg)}"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args.field, args.limbs if args.limbs != 1 else 1, args.cpu_log_n)
