@@ -57,6 +57,12 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
 
 /* Plan flags for the _ex constructors. */
 #define NTT_PLAN_TWIDDLE_ONLY 1u /* only the w_n tables: fill / twiddle_pack / transpose, no transforms */
+/* Elements are in Montgomery form x R mod p, R = 2^(64 limbs64) (CGBN's bn2mont domain,
+ * impl_cuda.cu:980-1010; the form arkworks / sppark / ICICLE callers keep their data in).  The
+ * transforms are linear, so forward / inverse / coset are unchanged (NTT(x R) = NTT(x) R); the
+ * pointwise product becomes the Montgomery product a b R^-1 so that polymul maps (a R, b R) to
+ * (a b) R.  Saves the caller a to/from-Montgomery pass over the data on each side. */
+#define NTT_PLAN_MONTGOMERY_IO 2u
 int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags);
 
 /* Modulus-generic plan, like big-num.cu's `prime` / `omega` kernel arguments (big-num.cu:68,173,260):
@@ -75,7 +81,16 @@ int ntt_inverse(ntt_plan* plan, void* d_data, void* hip_stream);
 int ntt_forward_batch(ntt_plan* plan, void* d_data, unsigned batch, void* hip_stream);
 int ntt_inverse_batch(ntt_plan* plan, void* d_data, unsigned batch, void* hip_stream);
 
-/* Pointwise product c = a * b mod p over 2^log_n elements (polynomial-multiply middle step). */
+/* Coset NTT, the low-degree-extension step of the GZKP provers the reference targets:
+ *   forward:  X_k = sum_j x_j (c w^k)^j = NTT(x_j c^j)          (evaluations on the coset c<w>)
+ *   inverse:  x_j = c^-j INTT(X)_j                               (interpolation from the coset)
+ * `shift` = c as limbs64 little-endian 64-bit limbs, canonical and nonzero (e.g. the field's
+ * multiplicative generator).  The plan caches the c^j tables of the last shift. */
+int ntt_forward_coset(ntt_plan* plan, void* d_data, const uint64_t* shift, void* hip_stream);
+int ntt_inverse_coset(ntt_plan* plan, void* d_data, const uint64_t* shift, void* hip_stream);
+
+/* Pointwise product c = a * b mod p over 2^log_n elements (polynomial-multiply middle step);
+ * a b R^-1 with NTT_PLAN_MONTGOMERY_IO. */
 int ntt_pointwise_mul(ntt_plan* plan, const void* d_a, const void* d_b, void* d_c, void* hip_stream);
 /* Cyclic polynomial product c = a * b of length 2^log_n: forward(a), forward(b), pointwise, inverse.
  * a and b are overwritten with their transforms. */

@@ -58,6 +58,10 @@ hipError_t launch_twiddle_pack(const uint32_t* src, uint32_t* dst, uint32_t log_
                                uint32_t lo_bits, const typename E::Args& F, hipStream_t st);
 template <class E>
 hipError_t launch_transpose(const uint32_t* src, uint32_t* dst, uint32_t log_rows, uint32_t log_cols, hipStream_t st);
+// data[j] *= c^j (coset / low-degree-extension scale), c^j = lo_s[j & mask] * hi[j >> lo_bits]
+template <class E>
+hipError_t launch_scale_pow(uint32_t* data, uint32_t log_n, uint32_t batch, const uint32_t* lo_s, const uint32_t* hi,
+                            uint32_t lo_bits, const typename E::Args& F, hipStream_t st);
 // c = a * b (canonical in/out): mont(mont(a, b), R^2) with r2 in the engine table format
 template <class E>
 hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, size_t n, const typename E::Args& F,

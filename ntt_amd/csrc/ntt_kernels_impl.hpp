@@ -433,6 +433,36 @@ __global__ void k_twiddle_pack(const uint32_t* __restrict__ src, uint32_t* __res
   E::template store<E::MUL_OUT>(dst, (blk << (log_rows + log_bw)) + (a << log_bw) + off, x, F);
 }
 
+// Coset scale (low-degree-extension step): data[j] *= c^j over `batch` vectors of 2^log_n elements,
+// c^j from two-level tables (lo_s[j & mask] = c^lo R_e, hi[j >> lo_bits] = Shoup entries), so
+// t = lo_s * hi = c^j R_e and mulv(x, t) = x c^j.  One HBM read + write, two products per element.
+template <class E>
+__global__ void k_scale_pow(uint32_t* __restrict__ data, uint32_t log_n, const uint32_t* __restrict__ lo_s,
+                            const uint32_t* __restrict__ hi, uint32_t lo_bits, const typename E::Args F,
+                            size_t batch_stride) {
+  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >> log_n) return;
+  uint32_t* d = data + (size_t)blockIdx.y * batch_stride;
+  uint32_t x[E::W];
+  typename E::Tw w, h;
+  E::load(x, d, j);
+  E::tload(w, lo_s, (uint32_t)(j & ((1ull << lo_bits) - 1)));
+  E::tload(h, hi, (uint32_t)(j >> lo_bits));
+  E::mul(w.w, h, F);
+  E::mulv(x, w.w, F);
+  E::template store<E::MUL_OUT>(d, j, x, F);
+}
+
+template <class E>
+hipError_t launch_scale_pow(uint32_t* data, uint32_t log_n, uint32_t batch, const uint32_t* lo_s, const uint32_t* hi,
+                            uint32_t lo_bits, const typename E::Args& F, hipStream_t st) {
+  const size_t n = 1ull << log_n;
+  const dim3 grid((uint32_t)((n + 255) / 256), batch);
+  hipLaunchKernelGGL((k_scale_pow<E>), grid, dim3(256), 0, st, data, log_n, lo_s, hi, lo_bits, F,
+                     n * (size_t)E::MEMW);
+  return hipGetLastError();
+}
+
 // dst[c][r] = src[r][c] for a rows x cols matrix of MEMW-word elements (32x32 tiles through LDS).
 template <int MEMW>
 __global__ void k_transpose(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t log_rows,
@@ -669,6 +699,8 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
   template hipError_t launch_pointwise<E>(const uint32_t*, const uint32_t*, uint32_t*, size_t,                     \
                                           const typename E::Args&, const uint32_t*, hipStream_t);                  \
   template hipError_t launch_build_tw<E>(uint32_t*, size_t, uint32_t, uint32_t, const uint32_t*, const uint32_t*,  \
-                                         uint32_t, const typename E::Args&, hipStream_t);
+                                         uint32_t, const typename E::Args&, hipStream_t);                          \
+  template hipError_t launch_scale_pow<E>(uint32_t*, uint32_t, uint32_t, const uint32_t*, const uint32_t*, uint32_t, \
+                                          const typename E::Args&, hipStream_t);
 
 }  // namespace ntt

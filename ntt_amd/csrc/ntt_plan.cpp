@@ -87,6 +87,7 @@ struct PlanBase {
   virtual int twiddle_pack(const void* src, void* dst, unsigned log_rows, unsigned log_len, unsigned log_bw,
                            uint64_t row0, bool inverse, hipStream_t st) = 0;
   virtual int transpose(const void* src, void* dst, unsigned log_rows, unsigned log_cols, hipStream_t st) = 0;
+  virtual int coset(void* d, const uint64_t* shift, unsigned limbs64, bool inverse, hipStream_t st) = 0;
   uint64_t n = 0;
   unsigned flags = 0;
   unsigned log_n = 0, elem_bytes = 0, npass = 0;
@@ -256,6 +257,7 @@ struct PlanImpl final : PlanBase {
   size_t off_int_f[8] = {0}, off_int_i[8] = {0};
   size_t off_lo_f = 0, off_hi_f = 0, off_lo_i = 0, off_hi_i = 0, off_hi_is = 0, off_r2 = 0;
   size_t off_los_f = 0, off_los_i = 0;  // lo tables scaled by R_e (left factor of on-the-fly twiddles)
+  size_t off_rm = 0;                    // R_e R^-1 (Montgomery-form pointwise product)
   unsigned lo_bits = 0;
   uint32_t nrand = 1, top_bits = 28;
 
@@ -266,6 +268,7 @@ struct PlanImpl final : PlanBase {
     if (d_tab) hipFree(d_tab);
     if (d_scratch) hipFree(d_scratch);
     if (d_full) hipFree(d_full);
+    if (d_coset) hipFree(d_coset);
     for (auto& row : ev)
       for (auto& e : row)
         if (e) hipEventDestroy(e);
@@ -369,19 +372,7 @@ struct PlanImpl final : PlanBase {
     std::vector<uint32_t> host;
     auto push_powers = [&](const Vec<NH>& base_m, uint64_t count, const Vec<NH>* scale_m,
                            bool scaled = false) -> size_t {
-      const size_t off = host.size();
-      Vec<NH> cur = scale_m ? *scale_m : H.r1;
-      uint32_t enc[TW];
-      for (uint64_t k = 0; k < count; ++k) {
-        if (scaled)
-          EH.encode_scaled(H.from_mont(cur), enc);
-        else
-          EH.encode(H.from_mont(cur), enc);
-        host.insert(host.end(), enc, enc + TW);
-        cur = H.mul(cur, base_m);
-      }
-      while (host.size() % 4) host.push_back(0);
-      return off;
+      return push_powers_to(host, base_m, count, scale_m, scaled);
     };
     const Vec<NH> ninv_m = H.to_mont(ninv_c);
     for (int dir = 0; dir < 2; ++dir) {
@@ -412,13 +403,23 @@ struct PlanImpl final : PlanBase {
         }
       }
     }
-    {  // R_e^2 mod p for the pointwise product = encode(R_e mod p), R_e the engine's Montgomery radix
+    {  // pointwise product constants: mulv leaves a b / R_e (R_e the engine's Montgomery radix);
+       // multiplying by R_e gives a b, by R_e R^-1 the Montgomery product a b R^-1 (R = 2^(64 limbs64))
       off_r2 = host.size();
       uint32_t enc[TW];
       EH.encode(engine_radix_mod_p(), enc);
       host.insert(host.end(), enc, enc + TW);
       while (host.size() % 4) host.push_back(0);
+      Vec<NH> rio{};  // R = 2^(64 limbs64) mod p by doubling
+      rio[0] = 1;
+      for (int k = 0; k < 64 * ((NH + 1) / 2); ++k) rio = H.add(rio, rio);
+      const Vec<NH> rio_inv = H.from_mont(H.pow(H.to_mont(rio), pm2));
+      off_rm = host.size();
+      EH.encode(H.from_mont(H.mul(H.to_mont(engine_radix_mod_p()), H.to_mont(rio_inv))), enc);
+      host.insert(host.end(), enc, enc + TW);
+      while (host.size() % 4) host.push_back(0);
     }
+    pm2_ = pm2;
     int cur = 0;
     hipGetDevice(&cur);
     if (hipSetDevice(device) != hipSuccess) return NTT_ERR_HIP;
@@ -462,6 +463,74 @@ struct PlanImpl final : PlanBase {
     if (hipDeviceSynchronize() != hipSuccess) return NTT_ERR_HIP;
     use_full = true;
     return NTT_OK;
+  }
+
+  // Append count entries base^k * scale (engine table format) to host; returns their word offset.
+  // scaled: entries hold value * R_e (the left factor of two-level products, see encode_scaled).
+  size_t push_powers_to(std::vector<uint32_t>& host, const Vec<NH>& base_m, uint64_t count, const Vec<NH>* scale_m,
+                        bool scaled) const {
+    const size_t off = host.size();
+    Vec<NH> cur = scale_m ? *scale_m : H.r1;
+    uint32_t enc[TW];
+    for (uint64_t k = 0; k < count; ++k) {
+      if (scaled)
+        EH.encode_scaled(H.from_mont(cur), enc);
+      else
+        EH.encode(H.from_mont(cur), enc);
+      host.insert(host.end(), enc, enc + TW);
+      cur = H.mul(cur, base_m);
+    }
+    while (host.size() % 4) host.push_back(0);
+    return off;
+  }
+
+  // ---- coset (low-degree extension): data[j] *= c^j before the forward, c^-j after the inverse
+  std::vector<uint32_t> coset_key;  // shift c (NH words) of the cached tables
+  uint32_t* d_coset = nullptr;
+  size_t coset_off[2][2] = {};  // [dir][lo_s, hi] word offsets into d_coset
+  std::vector<uint32_t> pm2_;    // p - 2 (inversion exponent)
+
+  int coset(void* d, const uint64_t* shift, unsigned limbs64, bool inverse, hipStream_t st) override {
+    if (!d || !shift || (flags & NTT_PLAN_TWIDDLE_ONLY)) return NTT_ERR_ARG;
+    Vec<NH> c{};
+    for (int i = 0; i < NH; ++i) c[i] = (uint32_t)(shift[i / 2] >> (32 * (i % 2)));
+    for (unsigned i = (NH + 1) / 2; i < limbs64; ++i)
+      if (shift[i]) return NTT_ERR_ARG;
+    if ((NH & 1) && (shift[NH / 2] >> 32)) return NTT_ERR_ARG;
+    Vec<NH> pv;
+    for (int i = 0; i < NH; ++i) pv[i] = H.M.p[i];
+    if (!vec_lt<NH>(c, pv) || c == Vec<NH>{}) return NTT_ERR_ARG;
+    const std::vector<uint32_t> key(c.begin(), c.end());
+    if (key != coset_key) {
+      if (d_coset) hipFree(d_coset);
+      d_coset = nullptr;
+      coset_key.clear();
+      std::vector<uint32_t> host;
+      const Vec<NH> cm = H.to_mont(c);
+      const Vec<NH> cim = H.pow(cm, pm2_);
+      for (int dir = 0; dir < 2; ++dir) {
+        const Vec<NH>& b = dir ? cim : cm;
+        coset_off[dir][0] = push_powers_to(host, b, 1ull << lo_bits, nullptr, true);
+        const Vec<NH> step = H.pow_u64(b, 1ull << lo_bits);
+        coset_off[dir][1] = push_powers_to(host, step, 1ull << (log_n - lo_bits), nullptr, false);
+      }
+      if (hipMalloc(&d_coset, host.size() * 4) != hipSuccess) return NTT_ERR_HIP;
+      if (hipMemcpy(d_coset, host.data(), host.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return NTT_ERR_HIP;
+      coset_key = key;
+    }
+    const int dir = inverse ? 1 : 0;
+    auto scale = [&]() {
+      return launch_scale_pow<E>(static_cast<uint32_t*>(d), log_n, 1, d_coset + coset_off[dir][0],
+                                 d_coset + coset_off[dir][1], lo_bits, Ff, st) == hipSuccess
+                 ? NTT_OK
+                 : NTT_ERR_HIP;
+    };
+    if (!inverse) {
+      if (int rc = scale()) return rc;
+      return run(d, 1, false, st);
+    }
+    if (int rc = run(d, 1, true, st)) return rc;
+    return scale();
   }
 
   // canonical value of the engine's Montgomery radix R_e mod p
@@ -552,8 +621,9 @@ struct PlanImpl final : PlanBase {
 
   int pointwise(const void* a, const void* b, void* c, hipStream_t st) override {
     if (!a || !b || !c) return NTT_ERR_ARG;
+    const size_t off = (flags & NTT_PLAN_MONTGOMERY_IO) ? off_rm : off_r2;
     hipError_t e = launch_pointwise<E>(static_cast<const uint32_t*>(a), static_cast<const uint32_t*>(b),
-                                       static_cast<uint32_t*>(c), n, Ff, d_tab + off_r2, st);
+                                       static_cast<uint32_t*>(c), n, Ff, d_tab + off, st);
     return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
   }
 
@@ -686,6 +756,19 @@ int ntt_forward(ntt_plan* plan, void* d_data, void* s) { return run_plan(plan, d
 int ntt_inverse(ntt_plan* plan, void* d_data, void* s) { return run_plan(plan, d_data, 1, true, s); }
 int ntt_forward_batch(ntt_plan* plan, void* d_data, unsigned b, void* s) { return run_plan(plan, d_data, b, false, s); }
 int ntt_inverse_batch(ntt_plan* plan, void* d_data, unsigned b, void* s) { return run_plan(plan, d_data, b, true, s); }
+
+static int run_coset(ntt_plan* plan, void* d, const uint64_t* shift, bool inv, void* stream) {
+  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
+  int cur = 0;
+  hipGetDevice(&cur);
+  if (cur != plan->impl->device) hipSetDevice(plan->impl->device);
+  const unsigned limbs64 = plan->impl->elem_bytes >= 32 ? plan->impl->elem_bytes / 8 : 1;
+  int rc = plan->impl->coset(d, shift, limbs64, inv, static_cast<hipStream_t>(stream));
+  if (cur != plan->impl->device) hipSetDevice(cur);
+  return set_err(rc);
+}
+int ntt_forward_coset(ntt_plan* plan, void* d, const uint64_t* shift, void* s) { return run_coset(plan, d, shift, false, s); }
+int ntt_inverse_coset(ntt_plan* plan, void* d, const uint64_t* shift, void* s) { return run_coset(plan, d, shift, true, s); }
 
 int ntt_pointwise_mul(ntt_plan* plan, const void* a, const void* b, void* c, void* s) {
   if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);

@@ -18,6 +18,7 @@ NTT_FIELD_P469762049 = 0
 NTT_FIELD_BN254_FR = 1
 NTT_FIELD_BLS12_381_FR = 2
 NTT_PLAN_TWIDDLE_ONLY = 1
+NTT_PLAN_MONTGOMERY_IO = 2
 
 # Every symbol declared in include/ntt.h with its ctypes prototype: (restype, argtypes).
 _vp = C.c_void_p
@@ -30,6 +31,8 @@ PROTOTYPES = {
     "ntt_forward_batch": (C.c_int, [_vp, _vp, C.c_uint, _vp]),
     "ntt_inverse_batch": (C.c_int, [_vp, _vp, C.c_uint, _vp]),
     "ntt_pointwise_mul": (C.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "ntt_forward_coset": (C.c_int, [_vp, _vp, C.POINTER(C.c_uint64), _vp]),
+    "ntt_inverse_coset": (C.c_int, [_vp, _vp, C.POINTER(C.c_uint64), _vp]),
     "ntt_polymul": (C.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "ntt_fill": (C.c_int, [_vp, _vp, C.c_int, C.c_uint64, _vp]),
     "ntt_plan_info": (C.c_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint), C.POINTER(C.c_uint),

@@ -78,7 +78,8 @@ class NTTPlan:
     """
 
     def __init__(self, field_id: int = 1, log_n: int = 10, limbs64: int = 4, device: int = 0,
-                 modulus: Optional[int] = None, generator: Optional[int] = None, twiddle_only: bool = False):
+                 modulus: Optional[int] = None, generator: Optional[int] = None, twiddle_only: bool = False,
+                 montgomery_io: bool = False):
         self._lib = _L.load()
         self.log_n = int(log_n)
         self.n = 1 << self.log_n
@@ -90,7 +91,8 @@ class NTTPlan:
         else:
             self.p, self.g = int(modulus), int(generator)
         h = C.c_void_p()
-        flags = _L.NTT_PLAN_TWIDDLE_ONLY if twiddle_only else 0
+        flags = (_L.NTT_PLAN_TWIDDLE_ONLY if twiddle_only else 0) | (_L.NTT_PLAN_MONTGOMERY_IO if montgomery_io else 0)
+        self.montgomery_io = bool(montgomery_io)
         if modulus is None:
             st = self._lib.ntt_plan_create_ex(C.byref(h), int(field_id), self.log_n, self.limbs64, self.device, flags)
         else:
@@ -145,6 +147,22 @@ class NTTPlan:
         self._check_tensor(t, batch)
         _L.check(self._lib.ntt_inverse_batch(self._h, C.c_void_p(t.data_ptr()), int(batch),
                                              _stream_ptr(stream, t.device)), "ntt_inverse_batch")
+        return t
+
+    def forward_coset(self, t: torch.Tensor, shift: int, stream=None) -> torch.Tensor:
+        """Evaluations on the coset shift*<w>: X_k = sum_j x_j (shift w^k)^j (low-degree extension)."""
+        self._check_tensor(t)
+        _L.check(self._lib.ntt_forward_coset(self._h, C.c_void_p(t.data_ptr()),
+                                             _u64_array(int_to_limbs(int(shift), self.limbs64)),
+                                             _stream_ptr(stream, t.device)), "ntt_forward_coset")
+        return t
+
+    def inverse_coset(self, t: torch.Tensor, shift: int, stream=None) -> torch.Tensor:
+        """Interpolation from the coset shift*<w>: x_j = shift^-j INTT(X)_j."""
+        self._check_tensor(t)
+        _L.check(self._lib.ntt_inverse_coset(self._h, C.c_void_p(t.data_ptr()),
+                                             _u64_array(int_to_limbs(int(shift), self.limbs64)),
+                                             _stream_ptr(stream, t.device)), "ntt_inverse_coset")
         return t
 
     def pointwise_mul(self, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, stream=None) -> torch.Tensor:

@@ -15,6 +15,12 @@ reference's (tie-pilot-qxw/NTT) definition of the transform:
 * ``kat_xj``       — closed form for the reference's own input ``x_j = j`` (``GZKP-NTT.cu:1587``):
                      ``X_0 = n(n-1)/2``, ``X_k = n / (w^k - 1)``.
 * ``four_step``    — the multi-GPU row/column decomposition, used to check layouts.
+* ``coset_ntt`` / ``coset_intt`` / ``kat_coset_xj`` — the coset (low-degree-extension) transform of
+                     SURVEY §8f.3, which the reference does not have: evaluations on c<w>,
+                     ``X_k = sum_j x_j (c w^k)^j``; pinned by ``dft_direct`` and a closed form for
+                     ``x_j = j`` (parity unpinned by the reference itself).
+* ``to_mont`` / ``from_mont`` — CGBN's Montgomery domain ``x R mod p``, ``R = 2^(64 limbs64)``
+                     (``bn2mont`` / ``mont2bn``, ``impl_cuda.cu:980-1024``), for the Montgomery-form I/O flag.
 
 Parity pins (see tests/test_oracle.py): the closed-form KAT, the reference-run 2^26 outputs recorded
 in SURVEY.md §0.3, the twiddle constant hard-coded in ``src/twiddlecheck.py:11``, and golden vectors
@@ -202,6 +208,36 @@ def kat_xj(n: int, p: int, g: int, k: int) -> int:
         return n * (n - 1) // 2 % p
     w = root_of_unity(p, g, n)
     return n * pow((pow(w, k, p) - 1) % p, p - 2, p) % p
+
+
+def coset_ntt(x: Sequence[int], p: int, g: int, c: int) -> List[int]:
+    """X_k = sum_j x_j (c w^k)^j = NTT(x_j c^j) (evaluations on the coset c<w>)."""
+    return ntt_dit([v * pow(c, j, p) % p for j, v in enumerate(x)], p, g)
+
+
+def coset_intt(X: Sequence[int], p: int, g: int, c: int) -> List[int]:
+    """Inverse of coset_ntt: x_j = c^-j INTT(X)_j."""
+    ci = pow(c, p - 2, p)
+    return [v * pow(ci, j, p) % p for j, v in enumerate(intt(X, p, g))]
+
+
+def kat_coset_xj(n: int, p: int, g: int, c: int, k: int) -> int:
+    """Closed form of coset_ntt(x_j = j) at output k: sum_{j<n} j z^j with z = c w^k, z^n = c^n:
+    z (1 - n z^(n-1) + (n-1) z^n) / (1 - z)^2  (z != 1)."""
+    w = root_of_unity(p, g, n)
+    z = c * pow(w, k, p) % p
+    if z == 1:
+        return n * (n - 1) // 2 % p
+    num = z * (1 - n * pow(z, n - 1, p) + (n - 1) * pow(z, n, p)) % p
+    return num * pow((1 - z) ** 2 % p, p - 2, p) % p
+
+
+def to_mont(v: int, p: int, limbs64: int) -> int:
+    return v * pow(2, 64 * limbs64, p) % p
+
+
+def from_mont(v: int, p: int, limbs64: int) -> int:
+    return v * pow(pow(2, 64 * limbs64, p), p - 2, p) % p
 
 
 def four_step(x: Sequence[int], p: int, g: int, n1: int, n2: int) -> List[int]:
