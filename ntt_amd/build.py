@@ -23,7 +23,7 @@ LIB = os.path.join(HERE, "libntt" + (f"_{_TAG}" if _TAG else "") + ".so")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
 # slowest translation units first (the pool runs them in list order)
-SOURCES = [f"ntt_{e}_{k}.hip" for e in ("e384", "e256", "ep") for k in ("col", "single", "fin", "misc")]
+SOURCES = [f"ntt_{e}_{k}.hip" for e in ("e384", "e256", "e256w", "ep") for k in ("col", "single", "fin", "misc")]
 SOURCES.append("ntt_plan.cpp")
 ARCH = os.environ.get("NTT_OFFLOAD_ARCH", "gfx950")
 

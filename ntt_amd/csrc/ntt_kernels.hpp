@@ -14,7 +14,8 @@ __host__ __device__ constexpr int tile_log_w(int ldsw) { return ldsw <= 9 ? 11 :
 __host__ __device__ constexpr int tile_elems_w(int ldsw) { return 1 << tile_log_w(ldsw); }
 
 using Eng256 = Eng29<9, 8>;    // 4 x 64-bit limbs in HBM
-using Eng384 = Eng29<14, 12>;  // 6 x 64-bit limbs in HBM
+using Eng384 = Eng29<14, 12>;  // 6 x 64-bit limbs in HBM, moduli up to 2^383
+using Eng256w = Eng29<9, 12>;  // 6 x 64-bit limbs in HBM, moduli < 2^255 (256-bit arithmetic)
 using EngP = Eng32<1, 2>;      // P469762049, `long long` in HBM
 
 template <class E>

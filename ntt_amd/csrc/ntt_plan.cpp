@@ -165,8 +165,11 @@ struct EngHost<Eng29<L, W32>> {
   // entry whose value is c R_e (R_e = B): the left factor of the two-level twiddle products
   void encode_scaled(const Vec<NH>& c, uint32_t* out) const { encode(times_B(c), out); }
   bool check_modulus(const uint32_t* p) const {
-    // p < 2^(32*W32 - 1) so that 2p fits the HBM words and 32p < B = 2^(29L)
-    return (p[NH - 1] >> 31) == 0 && 29 * L >= 32 * NH - 1 + 5;
+    // 2p fits the HBM words (p < 2^(32 W32 - 1)) and 64p <= B = 2^(29L) (lazy bounds up to 33p)
+    int bits = 0;
+    for (int i = NH - 1; i >= 0; --i)
+      if (p[i]) { bits = 32 * i + 32 - __builtin_clz(p[i]); break; }
+    return bits <= 32 * NH - 1 && bits <= 29 * L - 6;
   }
   void fill_args(EA& A, const uint32_t* p, const Vec<NH>* w8, const Vec<NH>& ninv) const {
     uint32_t pw[NH];
@@ -436,8 +439,8 @@ struct PlanImpl final : PlanBase {
   // Full per-pass outer-twiddle tables: pass i needs N_i entries (N_1 = n, N_2 = n / R_1, ...),
   // streamed from HBM like the data in pass 1 and L2-resident afterwards.  They replace the
   // two-level lookup's extra Montgomery product per element.  Skipped when a direction's tables
-  // would exceed kFullTableMaxBytes (the two-level tables are then used).
-  static constexpr size_t kFullTableMaxBytes = 2ull << 30;
+  // would not fit (the two-level tables are then used).
+  // Cap: both directions together within a quarter of the free HBM at plan creation.
   int build_full_tables() {
     size_t elems = 0;
     unsigned blk = log_n;
@@ -446,7 +449,9 @@ struct PlanImpl final : PlanBase {
       elems += 1ull << blk;
       blk -= r[i];
     }
-    if (elems * MEMW * 4 > kFullTableMaxBytes) return NTT_OK;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return NTT_OK;
+    if (2 * elems * MEMW * 4 > free_b / 4) return NTT_OK;
     if (hipMalloc(&d_full, 2 * elems * MEMW * 4) != hipSuccess) return NTT_ERR_HIP;
     for (int dir = 0; dir < 2; ++dir) {
       blk = log_n;
@@ -688,9 +693,17 @@ static int make_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, const 
     rc = impl->init(p32, g32, log_n, device, flags);
     out = std::move(impl);
   } else if (limbs64 == 6) {
-    auto impl = std::make_unique<PlanImpl<Eng384>>();
-    rc = impl->init(p32, g32, log_n, device, flags);
-    out = std::move(impl);
+    // the 384-bit element layout: 256-bit arithmetic when the modulus allows it (BN254 Fr,
+    // BLS12-381 Fr: the upper two 64-bit limbs of every element are zero), 14 limbs otherwise
+    if (p64[4] == 0 && p64[5] == 0 && (p64[3] >> 63) == 0) {
+      auto impl = std::make_unique<PlanImpl<Eng256w>>();
+      rc = impl->init(p32, g32, log_n, device, flags);
+      out = std::move(impl);
+    } else {
+      auto impl = std::make_unique<PlanImpl<Eng384>>();
+      rc = impl->init(p32, g32, log_n, device, flags);
+      out = std::move(impl);
+    }
   } else {
     return NTT_ERR_ARG;
   }

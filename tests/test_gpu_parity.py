@@ -218,3 +218,59 @@ def test_batch_forward():
     n = 1 << log_n
     for s in range(batch):
         assert np.array_equal(got[s * n:(s + 1) * n], _oracle_forward(x[s * n:(s + 1) * n], fid, L))
+
+
+def _is_prime(n: int) -> bool:
+    if n < 2:
+        return False
+    for sp in (2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37):
+        if n % sp == 0:
+            return n == sp
+    d, s = n - 1, 0
+    while d % 2 == 0:
+        d, s = d // 2, s + 1
+    for a in (2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41):
+        x = pow(a, d, n)
+        if x in (1, n - 1):
+            continue
+        for _ in range(s - 1):
+            x = x * x % n
+            if x == n - 1:
+                break
+        else:
+            return False
+    return True
+
+
+def _big_ntt_prime(bits: int, two_adicity: int):
+    """Smallest prime p = k 2^v + 1 >= 2^(bits-1) and a quadratic non-residue g (so that
+    g^((p-1)/n) is a primitive n-th root for every n | 2^v)."""
+    k = (1 << (bits - 1 - two_adicity)) + 1
+    while True:
+        p = k * (1 << two_adicity) + 1
+        if _is_prime(p):
+            break
+        k += 2
+    g = 2
+    while pow(g, (p - 1) // 2, p) != p - 1:
+        g += 1
+    return p, g
+
+
+@pytest.mark.parametrize("bits", [300, 380])
+def test_384bit_class_large_modulus_against_c_oracle(bits):
+    """Moduli above 2^255 take the 14-limb (406-bit) engine of the 6 x 64-bit layout (the 4-limb
+    class and the BN254 / BLS12-381 6-limb plans use the 9-limb engine): bit-exact vs the C oracle."""
+    from ntt_amd.ntt import NTTPlan
+    p, g = _big_ntt_prime(bits, 24)
+    rng = np.random.default_rng(bits)
+    for log_n in (3, 10, 12, 14):
+        n = 1 << log_n
+        vals = [int.from_bytes(rng.bytes(48), "little") % p for _ in range(n)]
+        x = OC.ints_to_limbs(vals, 6)
+        pl = NTTPlan(log_n=log_n, limbs64=6, modulus=p, generator=g)
+        t = _to_dev(x, 6)
+        pl.forward(t)
+        assert np.array_equal(_host(t, 6), OC.ntt_mp(x, p, g, False)), (bits, log_n)
+        pl.inverse(t)
+        assert np.array_equal(_host(t, 6), x), (bits, log_n)

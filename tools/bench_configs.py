@@ -1,0 +1,102 @@
+"""Time every BASELINE.json config that fits ONE MI355X (the headline is bench.py's job).
+
+    python tools/bench_configs.py [--out gpurun_out/configs.jsonl]
+
+One JSON line per config:
+  C2  2^20 forward, BN254 Fr (single-kernel-class size: 7+7+6 passes)
+  C3  2^24 forward + inverse, BLS12-381 Fr, 4- and 6-limb element layouts
+  C4  2^28 forward, BN254 Fr: on one GPU as a plain transform, and as the partitioned four-step
+      with 8 virtual ranks on one device (device copies stand in for the RCCL all-to-all; the
+      all-to-all over xGMI is timed only by bench.py --four-step on a multi-GPU node)
+  C5  polynomial multiply of length 2^24 (2 forward + pointwise + inverse), BN254 Fr
+  +   2^24 coset forward (low-degree extension), BN254 Fr
+Timing: W warmups, then K runs bracketed by torch.cuda.synchronize(); inputs resident in HBM.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fn, warmup=2, steps=10):
+    import torch
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default="gpurun_out/configs.jsonl")
+    args = ap.parse_args()
+    import torch
+    from ntt_amd.ntt import NTTPlan
+    from ntt_amd.distributed import VirtualRanks
+
+    rows = []
+
+    def emit(name, n, secs, **extra):
+        r = {"config": name, "n": n, "ms": secs * 1e3, "elements_per_s": n / secs, **extra}
+        rows.append(r)
+        print(json.dumps(r), flush=True)
+
+    # C2
+    pl = NTTPlan(1, 20, 4)
+    t = pl.fill(pl.empty(), "random", seed=2)
+    emit("C2: 2^20 forward BN254 Fr", 1 << 20, timeit(lambda: pl.forward(t), steps=50), passes=pl.passes)
+    del pl, t
+
+    # C3
+    for L in (4, 6):
+        pl = NTTPlan(2, 24, L)
+        t = pl.fill(pl.empty(), "random", seed=3)
+        emit(f"C3: 2^24 forward BLS12-381 Fr, {L}x64-bit limbs", 1 << 24, timeit(lambda: pl.forward(t)), passes=pl.passes)
+        emit(f"C3: 2^24 inverse BLS12-381 Fr, {L}x64-bit limbs", 1 << 24, timeit(lambda: pl.inverse(t)), passes=pl.passes)
+        emit(f"C3: 2^24 forward+inverse BLS12-381 Fr, {L}x64-bit limbs", 1 << 24,
+             timeit(lambda: (pl.forward(t), pl.inverse(t))), passes=pl.passes,
+             note="elements_per_s counts n per forward+inverse pair")
+        del pl, t
+        torch.cuda.empty_cache()
+
+    # C4
+    pl = NTTPlan(1, 28, 4)
+    t = pl.fill(pl.empty(), "random", seed=4)
+    emit("C4: 2^28 forward BN254 Fr, one GPU (plain transform)", 1 << 28, timeit(lambda: pl.forward(t), 1, 3),
+         passes=pl.passes)
+    del pl, t
+    torch.cuda.empty_cache()
+    vr = VirtualRanks(1, 28, 4, 8)
+    xs = vr.fill(vr.empty(), "random", seed=4)
+    emit("C4: 2^28 forward BN254 Fr, four-step over 8 virtual ranks on one GPU", 1 << 28,
+         timeit(lambda: vr.forward(xs), 1, 3),
+         note="exchange = device copies on one GPU; the RCCL all-to-all is timed by bench.py --four-step")
+    del vr, xs
+    torch.cuda.empty_cache()
+
+    # C5 and coset
+    pl = NTTPlan(1, 24, 4)
+    a = pl.fill(pl.empty(), "random", seed=5)
+    b = pl.fill(pl.empty(), "random", seed=6)
+    c = pl.empty()
+    emit("C5: polymul length 2^24 BN254 Fr (2 forward + pointwise + inverse), one GPU", 1 << 24,
+         timeit(lambda: pl.polymul(a, b, c)))
+    emit("coset forward 2^24 BN254 Fr (shift = generator 5)", 1 << 24, timeit(lambda: pl.forward_coset(a, 5)))
+
+    os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
+    with open(args.out, "w") as f:
+        for r in rows:
+            f.write(json.dumps(r) + "\n")
+
+
+if __name__ == "__main__":
+    main()
