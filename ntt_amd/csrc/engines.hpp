@@ -80,10 +80,12 @@ struct Eng29 {
     }
   }
   // x < 64p -> [0, 2p): x - q p with q = floor(x_top / (p_top + 1)) (float estimate biased low by
-  // 2^-10), which is floor(x / p) or one less when p_top >= 2^18.  x - q p = (x + q pbar) mod B.
-  // 9 MADs + ~30 simple ops instead of up to four conditional subtractions.
+  // 2^-15, more than its worst rounding overshoot 2^-17.9), which is floor(x / p) or one less when
+  // p_top >= 2^18; it is one less only when x / p is within ~2^-14 below an integer, so the result
+  // is < p for all but ~2^-14 of inputs.  x - q p = (x + q pbar) mod B.  9 MADs + ~30 simple ops
+  // instead of up to four conditional subtractions.
   __device__ static __forceinline__ void reduce_top(uint32_t (&x)[W], const Args& A) {
-    const float qf = __builtin_fmaf((float)x[L - 1], A.red_inv, -0x1p-10f);
+    const float qf = __builtin_fmaf((float)x[L - 1], A.red_inv, -0x1p-15f);
     const uint32_t q = qf > 0.f ? (uint32_t)qf : 0u;
     uint64_t acc = 0;
 #pragma unroll
@@ -95,11 +97,18 @@ struct Eng29 {
   // FAST (a kernel template flag, chosen per plan from Args::red_ok): quotient-estimate reduction
   // for the large drops.  A runtime branch here makes the compiler sink the two paths' kp[] uses into
   // one dynamically indexed access and copy the kernel arguments to scratch, hence the template.
+  // x < 2q (normalised) -> x < q, skipping the subtraction when no lane of the wave can need it
+  // (top limb below q's: x < q for sure).  Wave-uniform branch.
+  __device__ static __forceinline__ void cond_sub_rare(uint32_t (&x)[W], const uint32_t (&q)[L]) {
+    if (__any(x[L - 1] >= q[L - 1])) cond_sub<L>(x, q);
+  }
   template <int FROM, int TO, bool FAST = false>
   __device__ static __forceinline__ void reduce(uint32_t (&x)[W], const Args& A) {
     if constexpr (FAST && FROM > 4 && TO <= 4) {
       reduce_top(x, A);
-      if constexpr (TO == 1) cond_sub<L>(x, A.kp[0]);
+      if constexpr (TO == 1) cond_sub_rare(x, A.kp[0]);
+    } else if constexpr (FAST && FROM == 4 && TO == 2) {
+      cond_sub_rare(x, A.kp[1]);  // products: < 1.6p for BN254 Fr, < 2.4p for BLS12-381 Fr
     } else {
       reduce_chain<FROM, TO>(x, A);
     }
