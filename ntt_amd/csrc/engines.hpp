@@ -12,7 +12,15 @@
 #include "field29_asm9.hpp"
 
 #ifndef NTT_WAVES_256
-#define NTT_WAVES_256 2
+#define NTT_WAVES_256 4
+#endif
+// elements per thread in the pass kernels for the 256-bit class (4: radix-4 register sub-stages, 4
+// waves/SIMD; 8: radix-8 sub-stages, 2 waves/SIMD)
+#ifndef NTT_EPT_256
+#define NTT_EPT_256 4
+#endif
+#ifndef NTT_TILE_LOG_256
+#define NTT_TILE_LOG_256 10
 #endif
 
 namespace ntt {
@@ -34,10 +42,15 @@ struct Eng29 {
   static constexpr int LDSW = L;                // words per element in LDS
   static constexpr int IN = 4;                  // DFT input bound (units of p)
   static constexpr int MUL_OUT = 4;             // bound used for twiddle products (they are < 3p)
-  // pass-kernel occupancy target: 2 waves/SIMD (<= 256 VGPRs).  3 waves (<= 168 VGPRs, split LDS
-  // exchanges) spills ~300 B/thread with the Shoup operands live and measured 15 % slower.
-  static constexpr int WAVES_PER_EU = (L <= 9) ? NTT_WAVES_256 : 2;
-  static constexpr bool LDS_SPLIT = WAVES_PER_EU >= 3;
+  // Pass-kernel shape.  The products are long dependent v_mad_u64_u32 chains, so a SIMD needs 3-4
+  // resident waves to keep its VALU busy (Shoup product: 851 SIMD cycles at 2 waves, 785 at 3-4;
+  // profiles/r01_mb_mont29_v2.txt).  256-bit class: 4 elements per thread (radix-4 register
+  // sub-stages), 1024-element tiles (36 KiB LDS), 4 workgroups = 4 waves per SIMD.  384-bit class:
+  // 8 elements per thread, 1024-element tiles, 2 waves per SIMD.
+  static constexpr int EPT = (L <= 9) ? NTT_EPT_256 : 8;
+  static constexpr int TILE_LOG = (L <= 9) ? (EPT == 8 ? 11 : NTT_TILE_LOG_256) : 10;
+  static constexpr int WAVES_PER_EU = (L <= 9) ? (EPT == 4 ? NTT_WAVES_256 : 2) : 2;
+  static constexpr bool LDS_SPLIT = false;
   // quotient-estimate reduction needs p's top limb >= 2^18: possible only when 29L - 18 <= 255
   static constexpr bool FASTRED = 29 * L - 18 <= 255;
   struct Tw {
@@ -221,6 +234,8 @@ struct Eng32 {
   static constexpr int LDSW = N;
   static constexpr int IN = 4;
   static constexpr int MUL_OUT = 4;
+  static constexpr int EPT = 8;
+  static constexpr int TILE_LOG = (N <= 9) ? 11 : 10;
   static constexpr int WAVES_PER_EU = 4;
   static constexpr bool LDS_SPLIT = false;
   struct Tw {

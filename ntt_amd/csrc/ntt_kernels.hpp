@@ -8,10 +8,9 @@ namespace ntt {
 
 enum : int { KIND_COLUMN = 0, KIND_FINAL = 1, KIND_SINGLE = 2 };
 
-// Elements per workgroup tile: 2048 for <= 9-word elements (72 KiB LDS for the 29-bit 256-bit
-// class: two workgroups per CU), 1024 for the 384-bit class.
-__host__ __device__ constexpr int tile_log_w(int ldsw) { return ldsw <= 9 ? 11 : 10; }
-__host__ __device__ constexpr int tile_elems_w(int ldsw) { return 1 << tile_log_w(ldsw); }
+// Elements per workgroup tile of the multi-pass kernels (engines.hpp: E::TILE_LOG, E::EPT per thread).
+template <class E>
+__host__ __device__ constexpr int tile_log_of() { return E::TILE_LOG; }
 
 using Eng256 = Eng29<9, 8>;    // 4 x 64-bit limbs in HBM
 using Eng384 = Eng29<14, 12>;  // 6 x 64-bit limbs in HBM, moduli up to 2^383
@@ -44,8 +43,9 @@ template <class E>
 hipError_t launch_pass(int kind, int logr, const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t grid,
                        uint32_t batch, hipStream_t st);
 template <class E>
-hipError_t launch_build_tw(uint32_t* out, size_t count, uint32_t log_s, uint32_t log_m, const uint32_t* lo,
-                           const uint32_t* hi, uint32_t lo_bits, const typename E::Args& F, hipStream_t st);
+hipError_t launch_build_tw(uint32_t* out, size_t count, uint32_t log_r, uint32_t log_t, uint32_t log_m,
+                           const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits, const typename E::Args& F,
+                           hipStream_t st);
 template <class E>
 hipError_t launch_naive(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t batch, hipStream_t st);
 // Fill local element i with the synthetic value of global index

@@ -40,23 +40,27 @@ __host__ __device__ constexpr int brev_bits(int v, int bits) {
   return r;
 }
 
-template <int LOGR>
+// Sub-stage schedule of one radix-2^LOGR pass: register DFTs of radix 2^QB (QB = log2 of the
+// elements per thread), the last one smaller when QB does not divide LOGR.
+template <int LOGR, int QB>
 struct Sched {
-  static constexpr int nsub = (LOGR + 2) / 3;
-  static constexpr int qb(int s) { return (LOGR - 3 * s) >= 3 ? 3 : (LOGR - 3 * s); }
-  static constexpr int logN(int s) { return LOGR - 3 * s; }       // log2 N_s
+  static constexpr int nsub = (LOGR + QB - 1) / QB;
+  static constexpr int qb(int s) { return (LOGR - QB * s) >= QB ? QB : (LOGR - QB * s); }
+  static constexpr int logN(int s) { return LOGR - QB * s; }      // log2 N_s
   static constexpr int logsig(int s) { return logN(s) - qb(s); }  // log2 sigma_s
 };
+template <class E>
+constexpr int ept_log() { return E::EPT == 8 ? 3 : (E::EPT == 4 ? 2 : 1); }
 
 // natural index of in-workgroup position pi after all sub-stages (digit reversal)
-template <int LOGR>
+template <int LOGR, int QB>
 __device__ __forceinline__ uint32_t natural_index(uint32_t pi) {
-  using S = Sched<LOGR>;
+  using S = Sched<LOGR, QB>;
   uint32_t k = 0;
 #pragma unroll
   for (int s = 0; s < S::nsub; ++s) {
     const uint32_t ks = (pi >> S::logsig(s)) & ((1u << S::qb(s)) - 1);
-    k |= ks << (3 * s);
+    k |= ks << (QB * s);
   }
   return k;
 }
@@ -64,8 +68,8 @@ __device__ __forceinline__ uint32_t natural_index(uint32_t pi) {
 // In-register DFT of size Q in {2,4,8} over x[base + d], d < Q (DIF radix-2 network): output X_k
 // lands in slot base + brev(k).  Lazy bounds (engines.hpp): inputs < IN p, stage s offsets by
 // IN 2^(s-1) p, outputs < IN Q p.
-template <class E, int Q, int base>
-__device__ __forceinline__ void dft_q(uint32_t (&x)[8][E::W], const typename E::Args& F) {
+template <class E, int Q, int base, int N>
+__device__ __forceinline__ void dft_q(uint32_t (&x)[N][E::W], const typename E::Args& F) {
   constexpr int K1 = E::IN, K2 = 2 * E::IN, K3 = 4 * E::IN;
   if constexpr (Q == 2) {
     E::template bfly_l<K1>(x[base], x[base + 1], F);
@@ -99,8 +103,8 @@ __device__ __forceinline__ void dft_q(uint32_t (&x)[8][E::W], const typename E::
 //          normalise x0 x1 x2 x4 x6; stage 3 outputs <= (2^31, 33)
 //   Q = 4  stage 2 outputs <= (2.5 2^30, 17); Q = 2: (1.5 2^30, 9)
 // Products accept limbs < 2^31.6 (64-bit column sums) and values < B = 2^261 (33p < 2^260).
-template <class E, int Q, int base>
-__device__ __forceinline__ void dft_q_fast(uint32_t (&x)[8][E::W], const typename E::Args& F) {
+template <class E, int Q, int base, int N>
+__device__ __forceinline__ void dft_q_fast(uint32_t (&x)[N][E::W], const typename E::Args& F) {
   if constexpr (Q == 2) {
     E::template bfly_raw<E::PC_5_29>(x[base], x[base + 1], F);
   } else if constexpr (Q == 4) {
@@ -129,8 +133,8 @@ __device__ __forceinline__ void dft_q_fast(uint32_t (&x)[8][E::W], const typenam
     E::template bfly_raw<E::PC_4_29>(x[base + 6], x[base + 7], F);
   }
 }
-template <class E, int Q, int base, bool FAST>
-__device__ __forceinline__ void dft(uint32_t (&x)[8][E::W], const typename E::Args& F) {
+template <class E, int Q, int base, bool FAST, int N>
+__device__ __forceinline__ void dft(uint32_t (&x)[N][E::W], const typename E::Args& F) {
   if constexpr (FAST)
     dft_q_fast<E, Q, base>(x, F);
   else
@@ -155,11 +159,12 @@ __device__ __forceinline__ uint32_t lds_slot(uint32_t c, uint32_t pi) {
 
 // One LDS exchange + in-register radix-Q sub-stage s (s >= 1).
 template <class E, int LOGR, int T, int TE, int NT, int s, bool FAST>
-__device__ __forceinline__ void substage(uint32_t (&x)[8][E::W], uint32_t (&cl)[4], uint32_t (&pil)[4], uint32_t* lds,
-                                         const PassArgs<E>& A, int t) {
-  using S = Sched<LOGR>;
-  constexpr int pqb = S::qb(s - 1), PQ = 1 << pqb, PG = 8 / PQ, psb = S::logsig(s - 1), plN = S::logN(s - 1);
-  constexpr int qb = S::qb(s), Q = 1 << qb, G = 8 / Q, sb = S::logsig(s), lN = S::logN(s);
+__device__ __forceinline__ void substage(uint32_t (&x)[E::EPT][E::W], uint32_t (&cl)[E::EPT / 2],
+                                         uint32_t (&pil)[E::EPT / 2], uint32_t* lds, const PassArgs<E>& A, int t) {
+  using S = Sched<LOGR, ept_log<E>()>;
+  constexpr int EPT = E::EPT;
+  constexpr int pqb = S::qb(s - 1), PQ = 1 << pqb, PG = EPT / PQ, psb = S::logsig(s - 1), plN = S::logN(s - 1);
+  constexpr int qb = S::qb(s), Q = 1 << qb, G = EPT / Q, sb = S::logsig(s), lN = S::logN(s);
   using P = LdsParts<E::LDSW, E::LDS_SPLIT>;
   static_for<P::PARTS>([&](auto PT) {
     constexpr int part = PT;
@@ -208,14 +213,15 @@ __device__ __forceinline__ void substage(uint32_t (&x)[8][E::W], uint32_t (&cl)[
 }
 
 template <class E, int LOGR, int KIND, bool FULLTW, bool FAST>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
+__global__ __launch_bounds__((1 << E::TILE_LOG) / E::EPT) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
 void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                               const PassArgs<E> A) {
-  using S = Sched<LOGR>;
-  constexpr int TE = (KIND == KIND_SINGLE) ? (1 << LOGR) : tile_elems_w(E::LDSW);
+  constexpr int QB = ept_log<E>(), EPT = E::EPT;
+  using S = Sched<LOGR, QB>;
+  constexpr int TE = (KIND == KIND_SINGLE) ? (1 << LOGR) : (1 << tile_log_of<E>());
   constexpr int T = TE >> LOGR;  // columns (column pass) or blocks (final / single) per workgroup
-  constexpr int NT = TE / 8;     // threads
-  static_assert(LOGR >= 3 && T >= 1, "radix");
+  constexpr int NT = TE / EPT;   // threads
+  static_assert(LOGR >= QB && T >= 1, "radix");
   __shared__ __attribute__((aligned(16))) uint32_t lds[TE * LdsParts<E::LDSW, E::LDS_SPLIT>::max_words()];
 
   const int t = threadIdx.x;
@@ -248,13 +254,13 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
   }
   const uint32_t log_s = (KIND == KIND_COLUMN) ? (A.log_blk - LOGR) : 0u;
 
-  uint32_t x[8][E::W];
-  uint32_t cl[4];   // local column/block of each group (<= 4 groups per thread)
-  uint32_t pil[4];  // group index of each group
+  uint32_t x[EPT][E::W];
+  uint32_t cl[EPT / 2];   // local column/block of each group (<= EPT/2 groups per thread)
+  uint32_t pil[EPT / 2];  // group index of each group
 
   // ------------------------------------------------------------------ sub-stage 0: global -> regs
   {
-    constexpr int qb = S::qb(0), Q = 1 << qb, G = 8 / Q, sb = S::logsig(0);
+    constexpr int qb = S::qb(0), Q = 1 << qb, G = EPT / Q, sb = S::logsig(0);
     static_for<G>([&](auto J) {
       constexpr int j = J;
       const uint32_t lam = t + NT * j;
@@ -300,11 +306,14 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
   if constexpr (S::nsub > 1) substage<E, LOGR, T, TE, NT, 1, FAST>(x, cl, pil, lds, A, t);
   if constexpr (S::nsub > 2) substage<E, LOGR, T, TE, NT, 2, FAST>(x, cl, pil, lds, A, t);
   if constexpr (S::nsub > 3) substage<E, LOGR, T, TE, NT, 3, FAST>(x, cl, pil, lds, A, t);
+  if constexpr (S::nsub > 4) substage<E, LOGR, T, TE, NT, 4, FAST>(x, cl, pil, lds, A, t);
+  if constexpr (S::nsub > 5) substage<E, LOGR, T, TE, NT, 5, FAST>(x, cl, pil, lds, A, t);
+  static_assert(S::nsub <= 6, "sub-stages");
 
   // ------------------------------------------------------------------ output
   {
     constexpr int ls = S::nsub - 1;
-    constexpr int qb = S::qb(ls), Q = 1 << qb, G = 8 / Q, sb = S::logsig(ls), lN = S::logN(ls);
+    constexpr int qb = S::qb(ls), Q = 1 << qb, G = EPT / Q, sb = S::logsig(ls), lN = S::logN(ls);
     static_for<G>([&](auto J) {
       constexpr int j = J;
       const uint32_t g = pil[j];
@@ -314,15 +323,16 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
         constexpr int k = K;
         uint32_t(&v)[E::W] = x[j * Q + brev_bits(k, qb)];
         const uint32_t pi = (rho << lN) + cp + (k << sb);
-        const uint32_t kn = natural_index<LOGR>(pi);
+        const uint32_t kn = natural_index<LOGR, QB>(pi);
         size_t pos;
         if constexpr (KIND == KIND_COLUMN) {
           if constexpr (FULLTW) {
             // outer twiddle w_{N_i}^{col * kn} R_e from the per-pass table (HBM element format,
-            // indexed like the data within a block: HBM-streamed for pass 1, L2-resident later);
-            // the Montgomery product removes R_e.  32 B per entry instead of a 80-B Shoup pair.
+            // column-group-major [col / T][kn][col mod T], so one workgroup's entries are one
+            // contiguous T * R run: HBM-streamed for pass 1, L2-resident later); the Montgomery
+            // product removes R_e.  32 B per entry instead of a 80-B Shoup pair.
             uint32_t tw[E::W];
-            E::load(tw, A.tw_full, (size_t)(col0 + c) + ((size_t)kn << log_s));
+            E::load(tw, A.tw_full, ((size_t)col0 << LOGR) + (kn * T + c));
             E::mulv(v, tw, A.F);
           } else {
             // outer twiddle w_{N_i}^{col * kn} = w_n^{(col * kn) << log_m} from the two-level
@@ -381,16 +391,18 @@ __global__ void k_dft_naive(const uint32_t* __restrict__ src, uint32_t* __restri
   if (k < n) E::template store<E::IN>(dst + boff, k, acc, A.F);
 }
 
-// Per-pass outer-twiddle table: out[c + (k << log_s)] = w_n^((c*k) << log_m) R_e mod p (R_e the
-// engine's Montgomery radix), canonical in the HBM element format, built on the device from the
+// Per-pass outer-twiddle table of a column pass with radix 2^log_r and T = 2^log_t columns per
+// workgroup: entry (c, k) = w_n^((c*k) << log_m) R_e mod p (R_e the engine's Montgomery radix) at
+// [c >> log_t][k][c mod T], canonical in the HBM element format, built on the device from the
 // two-level tables (lo_s = lo R_e, so lo_s * hi = w R_e).
 template <class E>
-__global__ void k_build_tw(uint32_t* __restrict__ out, size_t count, uint32_t log_s, uint32_t log_m,
+__global__ void k_build_tw(uint32_t* __restrict__ out, size_t count, uint32_t log_r, uint32_t log_t, uint32_t log_m,
                            const uint32_t* __restrict__ lo, const uint32_t* __restrict__ hi, uint32_t lo_bits,
                            const typename E::Args F) {
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= count) return;
-  const size_t c = idx & ((1ull << log_s) - 1), k = idx >> log_s;
+  const size_t k = (idx >> log_t) & ((1ull << log_r) - 1);
+  const size_t c = ((idx >> (log_t + log_r)) << log_t) + (idx & ((1ull << log_t) - 1));
   const size_t e = (c * k) << log_m;
   typename E::Tw a, b;
   E::tload(a, lo, (uint32_t)(e & ((1ull << lo_bits) - 1)));
@@ -400,10 +412,11 @@ __global__ void k_build_tw(uint32_t* __restrict__ out, size_t count, uint32_t lo
 }
 
 template <class E>
-hipError_t launch_build_tw(uint32_t* out, size_t count, uint32_t log_s, uint32_t log_m, const uint32_t* lo,
-                           const uint32_t* hi, uint32_t lo_bits, const typename E::Args& F, hipStream_t st) {
-  hipLaunchKernelGGL((k_build_tw<E>), dim3((uint32_t)((count + 255) / 256)), dim3(256), 0, st, out, count, log_s,
-                     log_m, lo, hi, lo_bits, F);
+hipError_t launch_build_tw(uint32_t* out, size_t count, uint32_t log_r, uint32_t log_t, uint32_t log_m,
+                           const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits, const typename E::Args& F,
+                           hipStream_t st) {
+  hipLaunchKernelGGL((k_build_tw<E>), dim3((uint32_t)((count + 255) / 256)), dim3(256), 0, st, out, count, log_r,
+                     log_t, log_m, lo, hi, lo_bits, F);
   return hipGetLastError();
 }
 
@@ -592,13 +605,13 @@ __global__ void k_pointwise_mul(const uint32_t* __restrict__ a, const uint32_t* 
 template <class E, int KIND, int LOGR>
 static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t grid,
                                 uint32_t batch, hipStream_t st) {
-  constexpr int TL = tile_log_w(E::LDSW);
+  constexpr int TL = tile_log_of<E>();
   constexpr int MAXR = (KIND == KIND_SINGLE) ? TL : TL - 2;
   if constexpr (LOGR > MAXR) {
     return hipErrorInvalidValue;
   } else {
     constexpr int TE = (KIND == KIND_SINGLE) ? (1 << LOGR) : (1 << TL);
-    constexpr int NT = TE / 8;
+    constexpr int NT = TE / E::EPT;
     const dim3 g(grid, batch), b(NT < 64 ? 64 : NT);
     if constexpr (E::FASTRED) {
       if (A.F.red_ok) {
@@ -698,8 +711,8 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
   template hipError_t launch_transpose<E>(const uint32_t*, uint32_t*, uint32_t, uint32_t, hipStream_t);           \
   template hipError_t launch_pointwise<E>(const uint32_t*, const uint32_t*, uint32_t*, size_t,                     \
                                           const typename E::Args&, const uint32_t*, hipStream_t);                  \
-  template hipError_t launch_build_tw<E>(uint32_t*, size_t, uint32_t, uint32_t, const uint32_t*, const uint32_t*,  \
-                                         uint32_t, const typename E::Args&, hipStream_t);                          \
+  template hipError_t launch_build_tw<E>(uint32_t*, size_t, uint32_t, uint32_t, uint32_t, const uint32_t*,        \
+                                         const uint32_t*, uint32_t, const typename E::Args&, hipStream_t);         \
   template hipError_t launch_scale_pow<E>(uint32_t*, uint32_t, uint32_t, const uint32_t*, const uint32_t*, uint32_t, \
                                           const typename E::Args&, hipStream_t);
 

@@ -370,7 +370,7 @@ struct PlanImpl final : PlanBase {
     }
 
     // ---- schedule + tables (engine-encoded)
-    schedule(log_n, tile_log_w(E::LDSW), r, npass);
+    schedule(log_n, tile_log_of<E>(), r, npass);
     const bool twiddle_only = (flags & NTT_PLAN_TWIDDLE_ONLY) != 0;
     std::vector<uint32_t> host;
     auto push_powers = [&](const Vec<NH>& base_m, uint64_t count, const Vec<NH>* scale_m,
@@ -459,8 +459,9 @@ struct PlanImpl final : PlanBase {
         full_off[dir][i] = dir * elems + full_off[0][i];
         const uint32_t* lo = d_tab + (dir ? off_los_i : off_los_f);
         const uint32_t* hi = d_tab + (dir ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
-        if (launch_build_tw<E>(d_full + full_off[dir][i] * MEMW, 1ull << blk, blk - r[i], log_n - blk, lo, hi,
-                               lo_bits, dir ? Fi : Ff, nullptr) != hipSuccess)
+        // column-group-major layout of the pass kernel's tiles (T = TILE / R columns per workgroup)
+        if (launch_build_tw<E>(d_full + full_off[dir][i] * MEMW, 1ull << blk, r[i], tile_log_of<E>() - r[i],
+                               log_n - blk, lo, hi, lo_bits, dir ? Fi : Ff, nullptr) != hipSuccess)
           return NTT_ERR_HIP;
         blk -= r[i];
       }
@@ -589,7 +590,7 @@ struct PlanImpl final : PlanBase {
       mark(st);
     } else {
       if (int rc = ensure_scratch(batch)) return rc;
-      const uint32_t grid = (uint32_t)(n >> tile_log_w(E::LDSW));
+      const uint32_t grid = (uint32_t)(n >> tile_log_of<E>());
       unsigned blk = log_n;
       for (unsigned i = 0; i + 1 < npass && e == hipSuccess; ++i) {
         PassArgs<E> A = base_args(inverse);
