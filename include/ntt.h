@@ -92,8 +92,9 @@ int ntt_inverse_coset(ntt_plan* plan, void* d_data, const uint64_t* shift, void*
 /* Pointwise product c = a * b mod p over 2^log_n elements (polynomial-multiply middle step);
  * a b R^-1 with NTT_PLAN_MONTGOMERY_IO. */
 int ntt_pointwise_mul(ntt_plan* plan, const void* d_a, const void* d_b, void* d_c, void* hip_stream);
-/* Cyclic polynomial product c = a * b of length 2^log_n: forward(a), forward(b), pointwise, inverse.
- * a and b are overwritten with their transforms. */
+/* Cyclic polynomial product c = a * b of length 2^log_n: forward(a), forward(b), then the inverse
+ * of their pointwise product into c (multi-pass 256-bit plans fuse the pointwise product into the
+ * inverse's first pass).  a and b are overwritten with their transforms; c may alias a or b. */
 int ntt_polymul(ntt_plan* plan, void* d_a, void* d_b, void* d_c, void* hip_stream);
 
 /* Fill a device vector with the SURVEY §8d synthetic inputs: kind 0 = x_j = j (the reference's

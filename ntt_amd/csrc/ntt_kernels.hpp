@@ -24,6 +24,8 @@ struct PassArgs {
   const uint32_t* tw_lo;   // outer twiddles w_n^e = tw_lo[e mod 2^lo_bits] * tw_hi[e >> lo_bits]
   const uint32_t* tw_hi;
   const uint32_t* tw_full;  // column pass: per-pass outer twiddle table (HBM element format) or null
+  const uint32_t* src2;     // first column pass of a fused polymul inverse: x <- mont(src, src2) at load
+  const uint32_t* tw_in;    // first column pass of a fused coset forward: x_d <- x_d u^d (Shoup table, d < R)
   uint32_t lo_bits;
   uint32_t log_n;
   uint32_t log_blk;  // column pass: log2 of the block length N_i
@@ -45,7 +47,7 @@ hipError_t launch_pass(int kind, int logr, const uint32_t* src, uint32_t* dst, c
 template <class E>
 hipError_t launch_build_tw(uint32_t* out, size_t count, uint32_t log_r, uint32_t log_t, uint32_t log_m,
                            const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits, const typename E::Args& F,
-                           hipStream_t st);
+                           hipStream_t st, const uint32_t* clo = nullptr, const uint32_t* chi = nullptr);
 template <class E>
 hipError_t launch_naive(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t batch, hipStream_t st);
 // Fill local element i with the synthetic value of global index

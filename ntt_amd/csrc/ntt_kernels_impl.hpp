@@ -212,7 +212,15 @@ __device__ __forceinline__ void substage(uint32_t (&x)[E::EPT][E::W], uint32_t (
   });
 }
 
-template <class E, int LOGR, int KIND, bool FULLTW, bool FAST>
+// PRO: load prologue of a fused first column pass (FAST engines with full tables only).
+//   PRO_PW:    polynomial multiply.  The pass reads the two forward transforms src and A.src2 and
+//              starts from their Montgomery product a b / R_e; R_e is folded into the pass's
+//              outer-twiddle table together with n^-1 (PlanImpl::ensure_polymul_table).
+//   PRO_COSET: coset forward, x_j <- x_j c^j with j = col + s d: x_j u^d (u = c^s, Shoup table
+//              A.tw_in over the in-column index d) and c^col folded into the outer-twiddle table
+//              (PlanImpl::coset).
+enum : int { PRO_NONE = 0, PRO_PW = 1, PRO_COSET = 2 };
+template <class E, int LOGR, int KIND, bool FULLTW, bool FAST, int PRO = PRO_NONE>
 __global__ __launch_bounds__((1 << E::TILE_LOG) / E::EPT) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
 void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                               const PassArgs<E> A) {
@@ -287,6 +295,15 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
           pos = pi;
         }
         E::load(x[j * Q + d], src, pos);
+        if constexpr (PRO == PRO_PW) {
+          uint32_t y[E::W];
+          E::load(y, A.src2 + boff, pos);
+          E::mulv(x[j * Q + d], y, A.F);  // canonical inputs: < 3p, normalised
+        } else if constexpr (PRO == PRO_COSET) {
+          typename E::Tw u;
+          E::tload(u, A.tw_in, pi);
+          E::mul(x[j * Q + d], u, A.F);  // < 3p, normalised
+        }
       });
     });
     static_for<G>([&](auto J) {
@@ -394,11 +411,13 @@ __global__ void k_dft_naive(const uint32_t* __restrict__ src, uint32_t* __restri
 // Per-pass outer-twiddle table of a column pass with radix 2^log_r and T = 2^log_t columns per
 // workgroup: entry (c, k) = w_n^((c*k) << log_m) R_e mod p (R_e the engine's Montgomery radix) at
 // [c >> log_t][k][c mod T], canonical in the HBM element format, built on the device from the
-// two-level tables (lo_s = lo R_e, so lo_s * hi = w R_e).
+// two-level tables (lo_s = lo R_e, so lo_s * hi = w R_e).  With clo/chi (two-level tables of a coset
+// shift c in the same format) the entry is also multiplied by c^col.
 template <class E>
 __global__ void k_build_tw(uint32_t* __restrict__ out, size_t count, uint32_t log_r, uint32_t log_t, uint32_t log_m,
                            const uint32_t* __restrict__ lo, const uint32_t* __restrict__ hi, uint32_t lo_bits,
-                           const typename E::Args F) {
+                           const typename E::Args F, const uint32_t* __restrict__ clo,
+                           const uint32_t* __restrict__ chi) {
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= count) return;
   const size_t k = (idx >> log_t) & ((1ull << log_r) - 1);
@@ -408,15 +427,22 @@ __global__ void k_build_tw(uint32_t* __restrict__ out, size_t count, uint32_t lo
   E::tload(a, lo, (uint32_t)(e & ((1ull << lo_bits) - 1)));
   E::tload(b, hi, (uint32_t)(e >> lo_bits));
   E::mul(a.w, b, F);
+  if (clo) {  // c^col R_e = clo[col & mask] * chi[col >> lo_bits]; mulv removes one R_e
+    typename E::Tw u, v;
+    E::tload(u, clo, (uint32_t)(c & ((1ull << lo_bits) - 1)));
+    E::tload(v, chi, (uint32_t)(c >> lo_bits));
+    E::mul(u.w, v, F);
+    E::mulv(a.w, u.w, F);
+  }
   E::template store<E::MUL_OUT>(out, idx, a.w, F);
 }
 
 template <class E>
 hipError_t launch_build_tw(uint32_t* out, size_t count, uint32_t log_r, uint32_t log_t, uint32_t log_m,
                            const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits, const typename E::Args& F,
-                           hipStream_t st) {
+                           hipStream_t st, const uint32_t* clo, const uint32_t* chi) {
   hipLaunchKernelGGL((k_build_tw<E>), dim3((uint32_t)((count + 255) / 256)), dim3(256), 0, st, out, count, log_r,
-                     log_t, log_m, lo, hi, lo_bits, F);
+                     log_t, log_m, lo, hi, lo_bits, F, clo, chi);
   return hipGetLastError();
 }
 
@@ -616,15 +642,25 @@ static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassAr
     if constexpr (E::FASTRED) {
       if (A.F.red_ok) {
         if constexpr (KIND == KIND_COLUMN) {
+          if (A.tw_full && A.src2) {
+            hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true, true, PRO_PW>), g, b, 0, st, src, dst, A);
+            return hipGetLastError();
+          }
+          if (A.tw_full && A.tw_in) {
+            hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true, true, PRO_COSET>), g, b, 0, st, src, dst, A);
+            return hipGetLastError();
+          }
           if (A.tw_full) {
             hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true, true>), g, b, 0, st, src, dst, A);
             return hipGetLastError();
           }
         }
+        if (A.src2 || A.tw_in) return hipErrorInvalidValue;  // fused prologues: FAST column + full tables
         hipLaunchKernelGGL((k_pass<E, LOGR, KIND, false, true>), g, b, 0, st, src, dst, A);
         return hipGetLastError();
       }
     }
+    if (A.src2 || A.tw_in) return hipErrorInvalidValue;
     if constexpr (KIND == KIND_COLUMN) {
       if (A.tw_full) {
         hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true, false>), g, b, 0, st, src, dst, A);
@@ -712,7 +748,8 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
   template hipError_t launch_pointwise<E>(const uint32_t*, const uint32_t*, uint32_t*, size_t,                     \
                                           const typename E::Args&, const uint32_t*, hipStream_t);                  \
   template hipError_t launch_build_tw<E>(uint32_t*, size_t, uint32_t, uint32_t, uint32_t, const uint32_t*,        \
-                                         const uint32_t*, uint32_t, const typename E::Args&, hipStream_t);         \
+                                         const uint32_t*, uint32_t, const typename E::Args&, hipStream_t,          \
+                                         const uint32_t*, const uint32_t*);                                        \
   template hipError_t launch_scale_pow<E>(uint32_t*, uint32_t, uint32_t, const uint32_t*, const uint32_t*, uint32_t, \
                                           const typename E::Args&, hipStream_t);
 

@@ -82,6 +82,7 @@ struct PlanBase {
   virtual ~PlanBase() = default;
   virtual int run(void* d, unsigned batch, bool inverse, hipStream_t st) = 0;
   virtual int pointwise(const void* a, const void* b, void* c, hipStream_t st) = 0;
+  virtual int polymul(void* a, void* b, void* c, hipStream_t st) = 0;
   virtual int fill(void* d, uint64_t count, int kind, uint64_t seed, uint64_t row0, unsigned log_inner,
                    unsigned log_stride, hipStream_t st) = 0;
   virtual int twiddle_pack(const void* src, void* dst, unsigned log_rows, unsigned log_len, unsigned log_bw,
@@ -261,6 +262,8 @@ struct PlanImpl final : PlanBase {
   size_t off_lo_f = 0, off_hi_f = 0, off_lo_i = 0, off_hi_i = 0, off_hi_is = 0, off_r2 = 0;
   size_t off_los_f = 0, off_los_i = 0;  // lo tables scaled by R_e (left factor of on-the-fly twiddles)
   size_t off_rm = 0;                    // R_e R^-1 (Montgomery-form pointwise product)
+  size_t off_hi_ipm = 0;                // inverse hi table scaled by n^-1 R_e (fused polymul, pass 1)
+  uint32_t* d_full_pm = nullptr;        // inverse pass-1 outer twiddles x n^-1 R_e (fused polymul)
   unsigned lo_bits = 0;
   uint32_t nrand = 1, top_bits = 28;
 
@@ -271,7 +274,9 @@ struct PlanImpl final : PlanBase {
     if (d_tab) hipFree(d_tab);
     if (d_scratch) hipFree(d_scratch);
     if (d_full) hipFree(d_full);
+    if (d_full_pm) hipFree(d_full_pm);
     if (d_coset) hipFree(d_coset);
+    if (d_coset_full) hipFree(d_coset_full);
     for (auto& row : ev)
       for (auto& e : row)
         if (e) hipEventDestroy(e);
@@ -403,6 +408,9 @@ struct PlanImpl final : PlanBase {
           off_los_i = los;
           off_hi_i = hi;
           off_hi_is = push_powers(step, 1ull << (log_n - lo_bits), &ninv_m);
+          // fused polymul: the pointwise Montgomery product leaves a b / R_e; fold R_e in here
+          const Vec<NH> ninv_re_m = H.mul(ninv_m, H.to_mont(engine_radix_mod_p()));
+          off_hi_ipm = push_powers(step, 1ull << (log_n - lo_bits), &ninv_re_m);
         }
       }
     }
@@ -493,7 +501,9 @@ struct PlanImpl final : PlanBase {
   // ---- coset (low-degree extension): data[j] *= c^j before the forward, c^-j after the inverse
   std::vector<uint32_t> coset_key;  // shift c (NH words) of the cached tables
   uint32_t* d_coset = nullptr;
-  size_t coset_off[2][2] = {};  // [dir][lo_s, hi] word offsets into d_coset
+  uint32_t* d_coset_full = nullptr;  // fused coset forward: pass-1 outer twiddles x c^col (n entries)
+  bool coset_full_ok = false;
+  size_t coset_off[2][3] = {};  // [dir][lo_s, hi, u^d (forward only)] word offsets into d_coset
   std::vector<uint32_t> pm2_;    // p - 2 (inversion exponent)
 
   int coset(void* d, const uint64_t* shift, unsigned limbs64, bool inverse, hipStream_t st) override {
@@ -520,6 +530,9 @@ struct PlanImpl final : PlanBase {
         const Vec<NH> step = H.pow_u64(b, 1ull << lo_bits);
         coset_off[dir][1] = push_powers_to(host, step, 1ull << (log_n - lo_bits), nullptr, false);
       }
+      // fused forward: u^d, u = c^s (s = n / R_1 columns of pass 1), d < R_1, Shoup entries
+      if (npass >= 2) coset_off[0][2] = push_powers_to(host, H.pow_u64(cm, n >> r[0]), 1ull << r[0], nullptr, false);
+      coset_full_ok = false;
       if (hipMalloc(&d_coset, host.size() * 4) != hipSuccess) return NTT_ERR_HIP;
       if (hipMemcpy(d_coset, host.data(), host.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return NTT_ERR_HIP;
       coset_key = key;
@@ -532,11 +545,39 @@ struct PlanImpl final : PlanBase {
                  : NTT_ERR_HIP;
     };
     if (!inverse) {
+      if (coset_fusable()) {  // the scale rides in pass 1: u^d at load, c^col in the outer twiddles
+        if (int rc = ensure_coset_full()) return rc;
+        uint32_t* x = static_cast<uint32_t*>(d);
+        return run_io(x, nullptr, x, 1, false, st, d_coset_full, d_coset + coset_off[0][2]);
+      }
       if (int rc = scale()) return rc;
       return run(d, 1, false, st);
     }
     if (int rc = run(d, 1, true, st)) return rc;
     return scale();
+  }
+
+  bool coset_fusable() const {
+    if constexpr (!E::FASTRED) {
+      return false;
+    } else {
+      return use_full && npass >= 2 && Ff.red_ok;
+    }
+  }
+  // Pass-1 outer-twiddle table of the fused coset forward for the cached shift c: entry (col, k) =
+  // w_n^(col k) c^col R_e, layout of d_full (built on the device once per shift).
+  int ensure_coset_full() {
+    if (coset_full_ok) return NTT_OK;
+    if (!d_coset_full && hipMalloc(&d_coset_full, (size_t)n * MEMW * 4) != hipSuccess) {
+      d_coset_full = nullptr;
+      return NTT_ERR_HIP;
+    }
+    if (launch_build_tw<E>(d_coset_full, n, r[0], tile_log_of<E>() - r[0], 0, d_tab + off_los_f, d_tab + off_hi_f,
+                           lo_bits, Ff, nullptr, d_coset + coset_off[0][0], d_coset + coset_off[0][1]) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess)
+      return NTT_ERR_HIP;
+    coset_full_ok = true;
+    return NTT_OK;
   }
 
   // canonical value of the engine's Montgomery radix R_e mod p
@@ -571,8 +612,19 @@ struct PlanImpl final : PlanBase {
 
   int run(void* d, unsigned batch, bool inverse, hipStream_t st) override {
     if (!d || batch == 0 || (flags & NTT_PLAN_TWIDDLE_ONLY)) return NTT_ERR_ARG;
-    if (log_n == 0) return NTT_OK;
-    uint32_t* data = static_cast<uint32_t*>(d);
+    return run_io(static_cast<uint32_t*>(d), nullptr, static_cast<uint32_t*>(d), batch, inverse, st);
+  }
+
+  // One transform (or a batch): reads `in` (and, for a fused polymul inverse, `in2`: the first pass
+  // starts from the pointwise product in * in2), writes `out` (may equal `in`).
+  // Fused coset forward: full0 replaces the first pass's outer-twiddle table and tw_in scales its
+  // inputs (PRO_COSET in ntt_kernels_impl.hpp).
+  int run_io(const uint32_t* in, const uint32_t* in2, uint32_t* out, unsigned batch, bool inverse, hipStream_t st,
+             const uint32_t* full0 = nullptr, const uint32_t* tw_in = nullptr) {
+    if (log_n == 0) {
+      if (out != in) hipMemcpyAsync(out, in, (size_t)batch * MEMW * 4, hipMemcpyDeviceToDevice, st);
+      return NTT_OK;
+    }
     const size_t* off_int = inverse ? off_int_i : off_int_f;
     hipError_t e = hipSuccess;
     begin(st);
@@ -580,13 +632,13 @@ struct PlanImpl final : PlanBase {
       PassArgs<E> A = base_args(inverse);
       A.tw_int = d_tab + off_int[0];
       A.flags = inverse ? 1u : 0u;
-      e = launch_naive<E>(data, data, A, batch, st);
+      e = launch_naive<E>(in, out, A, batch, st);
       mark(st);
     } else if (npass == 1) {
       PassArgs<E> A = base_args(inverse);
       A.tw_int = d_tab + off_int[0];
       A.flags = inverse ? 1u : 0u;
-      e = launch_pass<E>(KIND_SINGLE, (int)r[0], data, data, A, 1, batch, st);
+      e = launch_pass<E>(KIND_SINGLE, (int)r[0], in, out, A, 1, batch, st);
       mark(st);
     } else {
       if (int rc = ensure_scratch(batch)) return rc;
@@ -598,9 +650,17 @@ struct PlanImpl final : PlanBase {
         A.tw_lo = d_tab + (inverse ? off_los_i : off_los_f);
         A.tw_hi = d_tab + (inverse ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
         A.tw_full = use_full ? d_full + full_off[inverse ? 1 : 0][i] * MEMW : nullptr;
+        if (i == 0 && in2) {
+          A.src2 = in2;
+          A.tw_full = d_full_pm;
+        }
+        if (i == 0 && tw_in) {
+          A.tw_in = tw_in;
+          A.tw_full = full0;
+        }
         A.log_blk = blk;
         A.log_m = log_n - blk;
-        const uint32_t* src = (i == 0) ? data : d_scratch;
+        const uint32_t* src = (i == 0) ? in : d_scratch;
         e = launch_pass<E>(KIND_COLUMN, (int)r[i], src, d_scratch, A, grid, batch, st);
         mark(st);
         blk -= r[i];
@@ -618,11 +678,50 @@ struct PlanImpl final : PlanBase {
           for (unsigned j = 1; j < idx; ++j) off += r[j];
           A.mid_off[m] = off;
         }
-        e = launch_pass<E>(KIND_FINAL, (int)r[npass - 1], d_scratch, data, A, grid, batch, st);
+        e = launch_pass<E>(KIND_FINAL, (int)r[npass - 1], d_scratch, out, A, grid, batch, st);
         mark(st);
       }
     }
     return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+  }
+
+  // Fused polymul is available for multi-pass FAST plans with full outer-twiddle tables.
+  bool polymul_fusable() const {
+    if constexpr (!E::FASTRED) {
+      return false;
+    } else {
+      return use_full && npass >= 2 && Fi.red_ok && !(flags & NTT_PLAN_MONTGOMERY_IO);
+    }
+  }
+  // Inverse pass-1 outer-twiddle table scaled by n^-1 R_e (built on first use, same layout as d_full).
+  int ensure_polymul_table() {
+    if (d_full_pm) return NTT_OK;
+    const size_t elems = 1ull << log_n;
+    if (hipMalloc(&d_full_pm, elems * MEMW * 4) != hipSuccess) {
+      d_full_pm = nullptr;
+      return NTT_ERR_HIP;
+    }
+    if (launch_build_tw<E>(d_full_pm, elems, r[0], tile_log_of<E>() - r[0], 0, d_tab + off_los_i,
+                           d_tab + off_hi_ipm, lo_bits, Fi, nullptr) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess)
+      return NTT_ERR_HIP;
+    return NTT_OK;
+  }
+
+  // c = a * b (cyclic convolution of length n): forward(a), forward(b) in place, then the inverse of
+  // their pointwise product into c.  Fused: the inverse's first pass reads both transforms and
+  // multiplies at load (one HBM pass and one kernel fewer than forward / pointwise / inverse).
+  int polymul(void* a, void* b, void* c, hipStream_t st) override {
+    if (!a || !b || !c || (flags & NTT_PLAN_TWIDDLE_ONLY)) return NTT_ERR_ARG;
+    uint32_t *pa = static_cast<uint32_t*>(a), *pb = static_cast<uint32_t*>(b), *pc = static_cast<uint32_t*>(c);
+    if (int rc = run_io(pa, nullptr, pa, 1, false, st)) return rc;
+    if (int rc = run_io(pb, nullptr, pb, 1, false, st)) return rc;
+    if (polymul_fusable()) {
+      if (int rc = ensure_polymul_table()) return rc;
+      return run_io(pa, pb, pc, 1, true, st);
+    }
+    if (int rc = pointwise(a, b, c, st)) return rc;
+    return run_io(pc, nullptr, pc, 1, true, st);
   }
 
   int pointwise(const void* a, const void* b, void* c, hipStream_t st) override {
@@ -790,10 +889,12 @@ int ntt_pointwise_mul(ntt_plan* plan, const void* a, const void* b, void* c, voi
 }
 
 int ntt_polymul(ntt_plan* plan, void* a, void* b, void* c, void* s) {
-  int rc = ntt_forward(plan, a, s);
-  if (rc == NTT_OK) rc = ntt_forward(plan, b, s);
-  if (rc == NTT_OK) rc = ntt_pointwise_mul(plan, a, b, c, s);
-  if (rc == NTT_OK) rc = ntt_inverse(plan, c, s);
+  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
+  int cur = 0;
+  hipGetDevice(&cur);
+  if (cur != plan->impl->device) hipSetDevice(plan->impl->device);
+  const int rc = plan->impl->polymul(a, b, c, static_cast<hipStream_t>(s));
+  if (cur != plan->impl->device) hipSetDevice(cur);
   return set_err(rc);
 }
 

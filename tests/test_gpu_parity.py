@@ -194,6 +194,45 @@ def test_polymul_matches_oracle():
     assert got == exp
 
 
+@pytest.mark.parametrize("fid,L,log_n", [(1, 4, 11), (1, 4, 16), (2, 4, 14), (2, 6, 13), (0, 4, 12), (0, 1, 13)])
+def test_polymul_sizes_and_aliasing(fid, L, log_n):
+    """Fused (multi-pass 256-bit plans: pointwise product inside the inverse's first pass) and
+    unfused polymul against the oracle; c aliasing a."""
+    p, g = R.FIELDS[fid]
+    pl = _plan(fid, log_n, L)
+    a, b = pl.empty(), pl.empty()
+    pl.fill(a, "random", seed=50 + log_n)
+    pl.fill(b, "random", seed=60 + log_n)
+    xa, xb = _host(a, L).copy(), _host(b, L).copy()
+    if L == 1:
+        A = OC.ntt_u64(xa[:, 0].astype(np.int64), p, g)
+        B = OC.ntt_u64(xb[:, 0].astype(np.int64), p, g)
+        C = np.array([(int(u) * int(v)) % p for u, v in zip(A, B)], dtype=np.int64)
+        exp = OC.ntt_u64(C, p, g, True).astype(np.uint64).reshape(-1, 1)
+    else:
+        exp = OC.ntt_mp(OC.mul_mp(OC.ntt_mp(xa, p, g), OC.ntt_mp(xb, p, g), p), p, g, inverse=True)
+    pl.polymul(a, b, a)  # c = a
+    assert np.array_equal(_host(a, L), exp), (fid, L, log_n, pl.passes)
+
+
+def test_polymul_full_size_shift():
+    """2^24 BN254 (BASELINE config 5 size): a * x = a cyclically shifted by one, a * 1 = a."""
+    fid, L, log_n = 1, 4, 24
+    pl = _plan(fid, log_n, L)
+    a, b, c = pl.empty(), pl.empty(), pl.empty()
+    pl.fill(a, "random", seed=5)
+    xa = _host(a, L).copy()
+    b.zero_()
+    b[1, 0] = 1
+    pl.polymul(a, b, c)
+    assert np.array_equal(_host(c, L), np.roll(xa, 1, axis=0))
+    pl.fill(a, "random", seed=5)
+    b.zero_()
+    b[0, 0] = 1
+    pl.polymul(a, b, c)
+    assert np.array_equal(_host(c, L), xa)
+
+
 def test_custom_modulus_matches_builtin():
     from ntt_amd.ntt import NTTPlan
     p, g = R.FIELDS[1]
