@@ -88,6 +88,93 @@ def gen_mont():
     return "\n".join(o)
 
 
+# ---------------------------------------------------------------- one asm statement per product
+# The column form above still pays hipcc's fixed boundary pad (an s_nop after every ;;#ASMEND whose
+# outputs a VALU reads next): ~17 per product.  Here the whole product, shifts and masks included, is
+# one statement, so the pad is paid once per product.  The 64-bit accumulator is the clobbered pair
+# v[ACC:ACC+1] (inline asm cannot name the low half of a 64-bit operand).  No wait states are
+# needed inside: every dependency is an ordinary VALU -> VALU one (no DPP / SDWA / op_sel / trans).
+ACC = 126
+MASK = "0x1fffffff"
+
+
+def _whole(lines, outs, ins, clobbers, indent="  "):
+    body = "\\n\\t".join(lines)
+    o = [f'{indent}asm("{body}"']
+    o.append(f"{indent}    : " + ", ".join(outs))
+    o.append(f"{indent}    : " + (",\n" + indent + "      ").join(", ".join(ins[i:i + 6]) for i in range(0, len(ins), 6)))
+    o.append(f"{indent}    : " + ", ".join(f'"{c}"' for c in clobbers) + ");")
+    return "\n".join(o)
+
+
+def gen_mulc_whole():
+    A = f"v[{ACC}:{ACC + 1}]"
+    R, Qo, CC, X, W, WS, PB = 0, L, 2 * L, 2 * L + 1, 3 * L + 1, 4 * L + 1, 5 * L + 1
+    lines = []
+    first = True
+    for K in range(L - 2, 2 * L - 1):  # q = floor(x * ws / B) from columns >= L-2
+        for i in range(max(0, K - (L - 1)), min(K, L - 1) + 1):
+            lines.append(f"v_mad_u64_u32 {A}, %{CC}, %{X + i}, %{WS + K - i}, {'0' if first else A}")
+            first = False
+        if K >= L:
+            lines.append(f"v_and_b32 %{Qo + K - L}, {MASK}, v{ACC}")
+        lines.append(f"v_lshrrev_b64 {A}, 29, {A}")
+    lines.append(f"v_mov_b32 %{Qo + L - 1}, v{ACC}")
+    for K in range(L):  # r = (x * w + q * pbar) mod B
+        for i in range(K + 1):
+            lines.append(f"v_mad_u64_u32 {A}, %{CC}, %{X + i}, %{W + K - i}, {'0' if K == 0 and i == 0 else A}")
+        for i in range(K + 1):
+            lines.append(f"v_mad_u64_u32 {A}, %{CC}, %{Qo + i}, %{PB + K - i}, {A}")
+        lines.append(f"v_and_b32 %{R + K}, {MASK}, v{ACC}")
+        if K + 1 < L:
+            lines.append(f"v_lshrrev_b64 {A}, 29, {A}")
+    outs = [f'"=&v"(r[{k}])' for k in range(L)] + [f'"=&v"(q[{k}])' for k in range(L)] + ['"=&s"(cc)']
+    ins = ([f'"v"(x[{k}])' for k in range(L)] + [f'"v"(w[{k}])' for k in range(L)] +
+           [f'"v"(ws[{k}])' for k in range(L)] + [f'"s"(pbar[{k}])' for k in range(L)])
+    o = ["__device__ __forceinline__ void mulc29_a9(uint32_t (&r)[9], const uint32_t (&x)[9], const uint32_t (&w)[9],",
+         "                                          const uint32_t (&ws)[9], const uint32_t (&pbar)[9]) {",
+         "  uint32_t q[9];",
+         "  uint64_t cc;",
+         _whole(lines, outs, ins, [f"v{ACC}", f"v{ACC + 1}"]),
+         "}"]
+    return "\n".join(o)
+
+
+def gen_mont_whole():
+    A = f"v[{ACC}:{ACC + 1}]"
+    R, Mo, CC, Ai, Bi, P, PINV = 0, L, 2 * L, 2 * L + 1, 3 * L + 1, 4 * L + 1, 5 * L + 1
+    lines = []
+    for i in range(L):
+        first = i == 0
+        for j in range(i + 1):
+            lines.append(f"v_mad_u64_u32 {A}, %{CC}, %{Ai + j}, %{Bi + i - j}, {'0' if first else A}")
+            first = False
+        for j in range(i):
+            lines.append(f"v_mad_u64_u32 {A}, %{CC}, %{Mo + j}, %{P + i - j}, {A}")
+        lines.append(f"v_mul_lo_u32 %{Mo + i}, v{ACC}, %{PINV}")
+        lines.append(f"v_and_b32 %{Mo + i}, {MASK}, %{Mo + i}")
+        lines.append(f"v_mad_u64_u32 {A}, %{CC}, %{Mo + i}, %{P}, {A}")
+        lines.append(f"v_lshrrev_b64 {A}, 29, {A}")
+    for i in range(L, 2 * L):
+        for j in range(i - L + 1, L):
+            lines.append(f"v_mad_u64_u32 {A}, %{CC}, %{Ai + j}, %{Bi + i - j}, {A}")
+        for j in range(i - L + 1, L):
+            lines.append(f"v_mad_u64_u32 {A}, %{CC}, %{Mo + j}, %{P + i - j}, {A}")
+        lines.append(f"v_and_b32 %{R + i - L}, {MASK}, v{ACC}")
+        if i + 1 < 2 * L:
+            lines.append(f"v_lshrrev_b64 {A}, 29, {A}")
+    outs = [f'"=&v"(r[{k}])' for k in range(L)] + [f'"=&v"(m[{k}])' for k in range(L)] + ['"=&s"(cc)']
+    ins = ([f'"v"(a[{k}])' for k in range(L)] + [f'"v"(b[{k}])' for k in range(L)] +
+           [f'"s"(M.p[{k}])' for k in range(L)] + ['"s"(M.pinv)'])
+    o = ["__device__ __forceinline__ void mont29_a9(uint32_t (&r)[9], const uint32_t (&a)[9], const uint32_t (&b)[9],",
+         "                                          const Mod29<9>& M) {",
+         "  uint32_t m[9];",
+         "  uint64_t cc;",
+         _whole(lines, outs, ins, [f"v{ACC}", f"v{ACC + 1}"]),
+         "}"]
+    return "\n".join(o)
+
+
 def main():
     print("// GENERATED by tools/gen_field29_asm.py -- do not edit.")
     print("// L = 9 radix-2^29 products (field29.hpp mulc29 / mont29) with one inline-asm MAD chain per")
@@ -96,7 +183,16 @@ def main():
     print('#include "field29.hpp"')
     print()
     print("namespace ntt {")
-    print("#if defined(__HIP_DEVICE_COMPILE__)")
+    print("#ifndef NTT_ASM_WHOLE")
+    print("#define NTT_ASM_WHOLE 0  // measured slower: 1.73 vs 1.67 ms (2^24 BN254; spills, no ILP across products)")
+    print("#endif")
+    print("#if defined(__HIP_DEVICE_COMPILE__) && NTT_ASM_WHOLE")
+    print("// one asm statement per product (see the generator)")
+    print(gen_mulc_whole())
+    print()
+    print(gen_mont_whole())
+    print("#elif defined(__HIP_DEVICE_COMPILE__)")
+    print("// one asm statement per product column")
     print(gen_mulc())
     print()
     print(gen_mont())
