@@ -40,13 +40,14 @@ SHOUP_MADS, MONT_MADS = 143, 162  # v_mad_u64_u32 per 256-bit product (field29.h
 
 
 def pass_mads(log_r: int, column: bool) -> float:
-    """v_mad_u64_u32 per element in one pass of radix 2^log_r (ntt_kernels_impl.hpp): radix-8/4/2
-    sub-stages with 5/8, 1/4, 0 internal products per element, (Q-1)/Q twiddle products between
-    sub-stages (Shoup), and in column passes one outer-twiddle Montgomery product."""
+    """v_mad_u64_u32 per element in one pass of radix 2^log_r (ntt_kernels_impl.hpp, 256-bit class:
+    4 elements per thread): radix-4/2 register sub-stages with 1/4, 0 internal products per element,
+    (Q-1)/Q twiddle products between sub-stages (Shoup), and in column passes one outer-twiddle
+    Montgomery product.  (Quotient-estimate reductions, 9 MADs each, are not counted.)"""
     subs, r = [], log_r
     while r > 0:
-        subs.append(min(3, r))
-        r -= min(3, r)
+        subs.append(min(2, r))
+        r -= min(2, r)
     internal = {3: 5 / 8, 2: 1 / 4, 1: 0.0}
     shoup = sum(internal[q] for q in subs) + sum((2 ** q - 1) / 2 ** q for q in subs[:-1])
     return shoup * SHOUP_MADS + (MONT_MADS if column else 0)
@@ -56,8 +57,10 @@ FIELD_NAMES = {0: "P469762049", 1: "BN254_FR", 2: "BLS12_381_FR"}
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    # the first ~20-30 transforms after start-up (or after >= 0.1 s idle) run 5-20 % slower while the
+    # GPU's clocks ramp (tools/exp_ramp.py, profiles/r01_v11/ramp.txt): the default warmup covers it
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--log-n", type=int, default=24)
     ap.add_argument("--field", type=int, default=1)
     ap.add_argument("--limbs", type=int, default=4)

@@ -23,7 +23,8 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def timeit(fn, warmup=2, steps=10):
+def timeit(fn, warmup=30, steps=20):
+    # warmup covers the GPU clock ramp (~20-30 transforms at 2^24, profiles/r01_v11/ramp.txt)
     import torch
     for _ in range(warmup):
         fn()
@@ -50,6 +51,14 @@ def main():
         rows.append(r)
         print(json.dumps(r), flush=True)
 
+    # the reference's own field and entry point: SSIP over P = 469762049, long long elements
+    for lg in (24, 26):
+        pl = NTTPlan(0, lg, 1)
+        t = pl.fill(pl.empty(), "random", seed=1)
+        emit(f"SSIP path: 2^{lg} forward P469762049 (reference field, 8-B elements)", 1 << lg,
+             timeit(lambda: pl.forward(t)), passes=pl.passes)
+        del pl, t
+
     # C2
     pl = NTTPlan(1, 20, 4)
     t = pl.fill(pl.empty(), "random", seed=2)
@@ -71,14 +80,14 @@ def main():
     # C4
     pl = NTTPlan(1, 28, 4)
     t = pl.fill(pl.empty(), "random", seed=4)
-    emit("C4: 2^28 forward BN254 Fr, one GPU (plain transform)", 1 << 28, timeit(lambda: pl.forward(t), 1, 3),
+    emit("C4: 2^28 forward BN254 Fr, one GPU (plain transform)", 1 << 28, timeit(lambda: pl.forward(t), 3, 5),
          passes=pl.passes)
     del pl, t
     torch.cuda.empty_cache()
     vr = VirtualRanks(1, 28, 4, 8)
     xs = vr.fill(vr.empty(), "random", seed=4)
     emit("C4: 2^28 forward BN254 Fr, four-step over 8 virtual ranks on one GPU", 1 << 28,
-         timeit(lambda: vr.forward(xs), 1, 3),
+         timeit(lambda: vr.forward(xs), 2, 3),
          note="exchange = device copies on one GPU; the RCCL all-to-all is timed by bench.py --four-step")
     del vr, xs
     torch.cuda.empty_cache()
@@ -88,6 +97,7 @@ def main():
     a = pl.fill(pl.empty(), "random", seed=5)
     b = pl.fill(pl.empty(), "random", seed=6)
     c = pl.empty()
+    emit("2^24 inverse BN254 Fr", 1 << 24, timeit(lambda: pl.inverse(a)), passes=pl.passes)
     emit("C5: polymul length 2^24 BN254 Fr (2 forward + pointwise + inverse), one GPU", 1 << 24,
          timeit(lambda: pl.polymul(a, b, c)))
     emit("coset forward 2^24 BN254 Fr (shift = generator 5)", 1 << 24, timeit(lambda: pl.forward_coset(a, 5)))
