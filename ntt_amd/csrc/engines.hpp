@@ -19,6 +19,18 @@
 #ifndef NTT_EPT_256
 #define NTT_EPT_256 4
 #endif
+#ifndef NTT_P_NARROW_FIRST
+#define NTT_P_NARROW_FIRST 1
+#endif
+#ifndef NTT_P_PASS1_TABLE
+#define NTT_P_PASS1_TABLE 0
+#endif
+#ifndef NTT_TILE_LOG_P
+#define NTT_TILE_LOG_P 13
+#endif
+#ifndef NTT_MIN_COLS_LOG_P
+#define NTT_MIN_COLS_LOG_P 4
+#endif
 #ifndef NTT_TILE_LOG_256
 #define NTT_TILE_LOG_256 10
 #endif
@@ -51,6 +63,8 @@ struct Eng29 {
   static constexpr int TILE_LOG = (L <= 9) ? (EPT == 8 ? 11 : NTT_TILE_LOG_256) : 10;
   static constexpr int WAVES_PER_EU = (L <= 9) ? (EPT == 4 ? NTT_WAVES_256 : 2) : 2;
   static constexpr bool LDS_SPLIT = false;
+  static constexpr int MIN_COLS_LOG = 2;  // column passes own >= 4 adjacent columns: >= 128-B runs
+  static constexpr bool PASS1_FULL_TABLE = true;  // VALU-bound: a table read beats a second product
   // quotient-estimate reduction needs p's top limb >= 2^18: possible only when 29L - 18 <= 255
   static constexpr bool FASTRED = 29 * L - 18 <= 255;
   struct Tw {
@@ -235,7 +249,14 @@ struct Eng32 {
   static constexpr int IN = 4;
   static constexpr int MUL_OUT = 4;
   static constexpr int EPT = 8;
-  static constexpr int TILE_LOG = (N <= 9) ? 11 : 10;
+  // 1-limb P path (8-B `long long` in HBM, 4-B words in LDS): 8192-element tiles (32 KiB LDS,
+  // 1024 threads) and >= 16 columns per column-pass workgroup, so every HBM run is >= 128 B;
+  // 2048-element tiles left 64-B runs at radix 256 and 32-B runs at radix 512 (2.0-3.3 TB/s).
+  static constexpr int TILE_LOG = (N == 1) ? NTT_TILE_LOG_P : ((N <= 9) ? 11 : 10);
+  static constexpr int MIN_COLS_LOG = (N == 1) ? NTT_MIN_COLS_LOG_P : 2;
+  // HBM-bound at 1 limb: pass 1 takes its outer twiddles from the two-level tables (2 cheap
+  // products) instead of streaming an n-entry table (+50 % pass-1 traffic)
+  static constexpr bool PASS1_FULL_TABLE = (N == 1) ? NTT_P_PASS1_TABLE : true;
   static constexpr int WAVES_PER_EU = 4;
   static constexpr bool LDS_SPLIT = false;
   struct Tw {

@@ -635,13 +635,13 @@ __global__ void k_pointwise_mul(const uint32_t* __restrict__ a, const uint32_t* 
 }
 
 // ---------------------------------------------------------------------------- launchers
-// Radices the planner can emit: column/final passes use 3 <= r <= tile_log - 2, single-workgroup
+// Radices the planner can emit: column/final passes use 3 <= r <= tile_log - MIN_COLS_LOG, single-workgroup
 // transforms 3 <= r <= tile_log.  Only those are instantiated.
 template <class E, int KIND, int LOGR>
 static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t grid,
                                 uint32_t batch, hipStream_t st) {
   constexpr int TL = tile_log_of<E>();
-  constexpr int MAXR = (KIND == KIND_SINGLE) ? TL : TL - 2;
+  constexpr int MAXR = (KIND == KIND_SINGLE) ? TL : TL - E::MIN_COLS_LOG;
   if constexpr (LOGR > MAXR) {
     return hipErrorInvalidValue;
   } else {
@@ -694,6 +694,8 @@ hipError_t launch_pass_kind(int logr, const uint32_t* src, uint32_t* dst, const 
     case 9: return launch_pass_r<E, KIND, 9>(src, dst, A, grid, batch, st);
     case 10: return launch_pass_r<E, KIND, 10>(src, dst, A, grid, batch, st);
     case 11: return launch_pass_r<E, KIND, 11>(src, dst, A, grid, batch, st);
+    case 12: return launch_pass_r<E, KIND, 12>(src, dst, A, grid, batch, st);
+    case 13: return launch_pass_r<E, KIND, 13>(src, dst, A, grid, batch, st);
     default: return hipErrorInvalidValue;
   }
 }

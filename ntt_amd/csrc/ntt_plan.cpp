@@ -9,6 +9,7 @@
 // Differences: tables are built once per plan (the reference rebuilt pq/omegas on every call and
 // freed them with a new[]/free mismatch, GZKP-NTT.cu:1554-1555); errors are returned as status
 // codes instead of asserts; nothing is printed.
+#include <algorithm>
 #include <hip/hip_runtime.h>
 
 #include <array>
@@ -112,16 +113,44 @@ struct PlanBase {
   }
 };
 
-// radices for log_n: near-equal split with each radix <= tile_log - 2 so that every global access
-// is a >= 4-element contiguous run (T = TILE / R >= 4).
-static void schedule(unsigned log_n, unsigned tile_log, unsigned* r, unsigned& p) {
-  if (log_n <= 2) { p = 0; return; }
-  if (log_n <= tile_log) { p = 1; r[0] = log_n; return; }
-  const unsigned rmax = tile_log - 2;
+// radices for log_n: near-equal split with each radix <= tile_log - min_cols_log so that every
+// global access is a contiguous run of T = TILE / R >= 2^min_cols_log elements (>= 128 B).
+// The pass kernels also need every column pass's block to span a whole tile (N_i = R_i ... R_p >=
+// TILE, so a workgroup's T columns lie in one block) and the final pass's T blocks to fit in R_1
+// (r_1 + r_p >= tile_log).  The near-equal split violates that only for short 3-pass schedules of
+// big tiles (2^19 on the 8192-element P tiles: 7+6+6); ascending order fixes every such case.
+static bool schedule_ok(const unsigned* r, unsigned p, unsigned tile_log) {
+  if (p < 2) return true;
+  if (r[0] + r[p - 1] < tile_log) return false;
+  unsigned tail = r[p - 1];
+  for (int i = (int)p - 2; i >= 0; --i) {
+    tail += r[i];
+    if (tail < tile_log) return false;
+  }
+  return true;
+}
+// narrow_first (HBM-bound engines): pass 1, whose columns are n / R_1 elements apart, takes a radix
+// one below the rest so that its workgroups read twice as wide runs (2^24 P: 7+8+9 instead of 8+8+8).
+static bool schedule(unsigned log_n, unsigned tile_log, unsigned min_cols_log, bool narrow_first, unsigned* r,
+                     unsigned& p) {
+  if (log_n <= 2) { p = 0; return true; }
+  if (log_n <= tile_log) { p = 1; r[0] = log_n; return true; }
+  const unsigned rmax = tile_log - min_cols_log;
   p = (log_n + rmax - 1) / rmax;
   if (p < 2) p = 2;
   const unsigned base = log_n / p, rem = log_n % p;
   for (unsigned i = 0; i < p; ++i) r[i] = base + (i < rem ? 1 : 0);
+  if (narrow_first) {
+    std::sort(r, r + p);
+    if (r[p - 1] < rmax && r[0] > 3) {
+      r[0] -= 1;
+      r[p - 1] += 1;
+      std::sort(r + 1, r + p);
+      if (!schedule_ok(r, p, tile_log)) { r[0] += 1; r[p - 1] -= 1; std::sort(r, r + p); }
+    }
+  }
+  if (!schedule_ok(r, p, tile_log)) std::sort(r, r + p);
+  return schedule_ok(r, p, tile_log);
 }
 
 // ------------------------------------------------------------------------------ engine encodings
@@ -375,7 +404,8 @@ struct PlanImpl final : PlanBase {
     }
 
     // ---- schedule + tables (engine-encoded)
-    schedule(log_n, tile_log_of<E>(), r, npass);
+    if (!schedule(log_n, tile_log_of<E>(), E::MIN_COLS_LOG, !E::PASS1_FULL_TABLE && NTT_P_NARROW_FIRST, r, npass))
+      return NTT_ERR_ARG;
     const bool twiddle_only = (flags & NTT_PLAN_TWIDDLE_ONLY) != 0;
     std::vector<uint32_t> host;
     auto push_powers = [&](const Vec<NH>& base_m, uint64_t count, const Vec<NH>* scale_m,
@@ -649,7 +679,9 @@ struct PlanImpl final : PlanBase {
         A.tw_int = d_tab + off_int[i];
         A.tw_lo = d_tab + (inverse ? off_los_i : off_los_f);
         A.tw_hi = d_tab + (inverse ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
-        A.tw_full = use_full ? d_full + full_off[inverse ? 1 : 0][i] * MEMW : nullptr;
+        // pass 1 of a memory-bound engine (8-B P path) computes its outer twiddles from the
+        // L2-resident two-level tables: two 32-bit products are cheaper than streaming an n-entry table
+        A.tw_full = (use_full && (i > 0 || E::PASS1_FULL_TABLE)) ? d_full + full_off[inverse ? 1 : 0][i] * MEMW : nullptr;
         if (i == 0 && in2) {
           A.src2 = in2;
           A.tw_full = d_full_pm;
