@@ -146,6 +146,24 @@ int NTT_GZKP_64(long long* data, const void* reverse, long long len, long long o
                 long long reverse_num);
 int ntt_last_error(void);
 
+/* ---------------------------------------------------------------- single-process multi-GPU
+ * New (the reference has no multi-GPU code).  One plan drives `ngpus` devices of one node (power of
+ * two); a transform is the four-step with ONE RCCL all-to-all over xGMI (ncclCommInitAll over
+ * `devices`).  d_data[g] / hip_streams[g] belong to devices[g] (streams may be NULL = default
+ * streams); each d_data[g] holds n / ngpus elements.  Layouts (as ntt_amd/distributed.py), with
+ * n1 = 2^ceil(log_n/2), n2 = 2^floor(log_n/2), r = n1/ngpus, c = n2/ngpus:
+ *   forward input  (row layout):    d_data[g] = [r][n2], element (a, j2) = x[g r + a + n1 j2]
+ *   forward output (column layout): d_data[g] = [c][n1], element (kc, k1) = X[g c + kc + n2 k1]
+ * The inverse takes the column layout back to the row layout (1/n included).  Asynchronous. */
+typedef struct ntt_mplan ntt_mplan;
+int ntt_mplan_create(ntt_mplan** out, int field_id, unsigned log_n, unsigned limbs64, int ngpus, const int* devices);
+int ntt_forward_multi(ntt_mplan* plan, void* const* d_data, void* const* hip_streams);
+int ntt_inverse_multi(ntt_mplan* plan, void* const* d_data, void* const* hip_streams);
+/* each device's row-layout share of the global synthetic vector (kinds as ntt_fill) */
+int ntt_mplan_fill(ntt_mplan* plan, void* const* d_data, int kind, uint64_t seed, void* const* hip_streams);
+int ntt_mplan_info(const ntt_mplan* plan, uint64_t* local_n, unsigned* log_n1, unsigned* log_n2);
+int ntt_mplan_destroy(ntt_mplan* plan);
+
 #ifdef __cplusplus
 }
 #endif

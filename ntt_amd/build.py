@@ -24,7 +24,7 @@ INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
 # slowest translation units first (the pool runs them in list order)
 SOURCES = [f"ntt_{e}_{k}.hip" for e in ("e384", "e256", "e256w", "ep") for k in ("col", "single", "fin", "misc")]
-SOURCES.append("ntt_plan.cpp")
+SOURCES += ["ntt_plan.cpp", "ntt_multi.cpp"]
 ARCH = os.environ.get("NTT_OFFLOAD_ARCH", "gfx950")
 
 
@@ -68,9 +68,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
         objs = list(ex.map(lambda s: _compile(s, hdr), srcs))
     if not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
         cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp", *objs]
-        rccl = "/opt/rocm/lib/librccl.so"
-        if os.path.exists(rccl):
-            cmd += ["-L/opt/rocm/lib", "-lrccl"]
+        cmd += ["-ldl"]  # RCCL is dlopen-ed by ntt_multi.cpp at first multi-GPU use
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")

@@ -246,3 +246,62 @@ class VirtualRanks:
         for fs, x in zip(self.ranks, xs):
             fs.inverse_phase2(x)
         return xs
+
+
+class MultiPlan:
+    """Single-process multi-GPU plan over the C ABI (``ntt_mplan_*``, ntt_amd/csrc/ntt_multi.cpp):
+    one process drives ``devices`` with the same four-step and layouts as DistNTT, the exchange
+    being one grouped RCCL all-to-all.  Shares are torch tensors, ``xs[g]`` on ``devices[g]``.
+    """
+
+    def __init__(self, field_id: int = 1, log_n: int = 24, limbs64: int = 4, devices: Optional[List[int]] = None):
+        import ctypes as C
+        from . import lib as _L
+        self._C, self._L = C, _L
+        self.lib = _L.load()
+        self.devices = list(devices if devices is not None else range(torch.cuda.device_count()))
+        self.limbs64 = limbs64
+        arr = (C.c_int * len(self.devices))(*self.devices)
+        h = C.c_void_p()
+        _L.check(self.lib.ntt_mplan_create(C.byref(h), field_id, log_n, limbs64, len(self.devices), arr),
+                 "ntt_mplan_create")
+        self.handle = h
+        local_n, n1, n2 = C.c_uint64(), C.c_uint(), C.c_uint()
+        self.lib.ntt_mplan_info(h, C.byref(local_n), C.byref(n1), C.byref(n2))
+        self.local_n, self.log_n1, self.log_n2 = local_n.value, n1.value, n2.value
+        self.layouts = [Layout(log_n, len(self.devices), g) for g in range(len(self.devices))]
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            self.lib.ntt_mplan_destroy(h)
+            self.handle = None
+
+    def empty(self) -> List[torch.Tensor]:
+        shape = (self.local_n,) if self.limbs64 == 1 else (self.local_n, self.limbs64)
+        return [torch.empty(shape, dtype=torch.int64, device=f"cuda:{d}") for d in self.devices]
+
+    def _ptrs(self, xs):
+        C = self._C
+        for t, d in zip(xs, self.devices):
+            if not t.is_contiguous() or t.device.index != d or t.numel() * 8 != self.local_n * 8 * self.limbs64:
+                raise ValueError("each share must be a contiguous tensor of local_n elements on its device")
+        data = (C.c_void_p * len(xs))(*[t.data_ptr() for t in xs])
+        streams = (C.c_void_p * len(xs))(*[torch.cuda.current_stream(d).cuda_stream for d in self.devices])
+        return data, streams
+
+    def fill(self, xs, kind: str = "random", seed: int = 1):
+        data, streams = self._ptrs(xs)
+        self._L.check(self.lib.ntt_mplan_fill(self.handle, data, 0 if kind == "iota" else 1, seed, streams),
+                      "ntt_mplan_fill")
+        return xs
+
+    def forward(self, xs):
+        data, streams = self._ptrs(xs)
+        self._L.check(self.lib.ntt_forward_multi(self.handle, data, streams), "ntt_forward_multi")
+        return xs
+
+    def inverse(self, xs):
+        data, streams = self._ptrs(xs)
+        self._L.check(self.lib.ntt_inverse_multi(self.handle, data, streams), "ntt_inverse_multi")
+        return xs

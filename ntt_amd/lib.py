@@ -52,6 +52,12 @@ PROTOTYPES = {
     "ntt_fill_map": (C.c_int, [_vp, _vp, C.c_uint64, C.c_int, C.c_uint64, C.c_uint64, C.c_uint, C.c_uint, _vp]),
     "ntt_twiddle_pack": (C.c_int, [_vp, _vp, _vp, C.c_uint, C.c_uint, C.c_uint, C.c_uint64, C.c_int, _vp]),
     "ntt_transpose": (C.c_int, [_vp, _vp, _vp, C.c_uint, C.c_uint, _vp]),
+    "ntt_mplan_create": (C.c_int, [C.POINTER(_vp), C.c_int, C.c_uint, C.c_uint, C.c_int, C.POINTER(C.c_int)]),
+    "ntt_forward_multi": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp)]),
+    "ntt_inverse_multi": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp)]),
+    "ntt_mplan_fill": (C.c_int, [_vp, C.POINTER(_vp), C.c_int, C.c_uint64, C.POINTER(_vp)]),
+    "ntt_mplan_info": (C.c_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint), C.POINTER(C.c_uint)]),
+    "ntt_mplan_destroy": (C.c_int, [_vp]),
 }
 
 _lock = threading.Lock()

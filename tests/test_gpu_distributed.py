@@ -67,3 +67,26 @@ def test_dist_ntt_rccl_world1():
         assert torch.equal(t, t0)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("log_n,field_id,L", [(12, 1, 4), (17, 1, 4), (16, 2, 6), (14, 0, 1)])
+def test_mplan_single_process_rccl(log_n, field_id, L):
+    """ntt_mplan_* (one process, ncclCommInitAll over the visible devices, grouped all-to-all):
+    the column-layout output equals the single-GPU transform; the inverse restores the rows."""
+    from ntt_amd.distributed import MultiPlan
+    from ntt_amd.ntt import NTTPlan
+    mp = MultiPlan(field_id, log_n, L, devices=list(range(torch.cuda.device_count())))
+    xs = mp.fill(mp.empty(), "random", seed=11)
+    ref = NTTPlan(field_id, log_n, L)
+    x = ref.fill(ref.empty(), "random", seed=11)
+    x0 = x.clone()
+    for lay, t in zip(mp.layouts, xs):
+        assert torch.equal(t.to("cuda:0"), x0[_index(lay, "row")])
+    shares = [t.clone() for t in xs]
+    ref.forward(x)
+    mp.forward(xs)
+    for lay, t in zip(mp.layouts, xs):
+        assert torch.equal(t.to("cuda:0"), x[_index(lay, "col")]), (log_n, lay.rank)
+    mp.inverse(xs)
+    for s, t in zip(shares, xs):
+        assert torch.equal(s, t)
