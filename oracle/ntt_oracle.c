@@ -259,6 +259,93 @@ int oracle_ntt_mp(uint64_t* data, uint32_t log_n, uint32_t limbs64, const uint64
   return 0;
 }
 
+/* The same transform with each stage's butterflies split over `threads` OpenMP threads (chunks of
+ * one block's offsets; a chunk starts from w = gap^off0).  Used only as the multi-core CPU baseline
+ * of bench.py; tests check it against oracle_ntt_mp. */
+int oracle_ntt_mp_par(uint64_t* data, uint32_t log_n, uint32_t limbs64, const uint64_t* p, const uint64_t* g,
+                      int inverse, int threads) {
+  mp_field F;
+  if (mp_field_init(&F, p, (int)limbs64)) return -1;
+  const int L = F.L;
+  const uint64_t n = 1ull << log_n;
+  uint64_t pm1[MAXL], gm[MAXL], one[MAXL] = {1};
+  mp_sub(pm1, p, one, L);
+  mp_to_mont(gm, g, &F);
+  if (inverse) {
+    uint64_t two[MAXL] = {2}, pm2[MAXL];
+    mp_sub(pm2, p, two, L);
+    mp_pow_mont(gm, gm, pm2, &F);
+  }
+  if (threads < 1) threads = 1;
+#pragma omp parallel for num_threads(threads) schedule(static)
+  for (uint64_t i = 0; i < n; i++) mp_to_mont(data + i * L, data + i * L, &F);
+  if (log_n) {
+    uint32_t* rev = (uint32_t*)calloc(n, sizeof(uint32_t));
+    for (uint64_t i = 1; i < n; i++) rev[i] = (rev[i >> 1] >> 1) | ((uint32_t)(i & 1) << (log_n - 1));
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (uint64_t i = 0; i < n; i++)
+      if (i < rev[i]) {
+        uint64_t tmp[MAXL];
+        memcpy(tmp, data + i * L, 8 * L);
+        memcpy(data + i * L, data + (uint64_t)rev[i] * L, 8 * L);
+        memcpy(data + (uint64_t)rev[i] * L, tmp, 8 * L);
+      }
+    free(rev);
+  }
+  const uint64_t chunk = 4096; /* butterflies per task */
+  for (uint64_t stride = 1, lg = 1; stride < n; stride <<= 1, lg++) {
+    uint64_t e[MAXL] = {0}, gap[MAXL];
+    for (int i = 0; i < L; i++) {
+      e[i] = pm1[i] >> lg;
+      if (i + 1 < L && lg) e[i] |= pm1[i + 1] << (64 - lg);
+    }
+    mp_pow_mont(gap, gm, e, &F);
+    /* a task = `bpt` whole blocks (short strides) or one `chunk`-offset slice of a block */
+    const uint64_t blocks = n / (2 * stride);
+    const uint64_t per_block = (stride + chunk - 1) / chunk;
+    const uint64_t bpt = stride >= chunk ? 1 : (chunk / stride < blocks ? chunk / stride : blocks);
+    const uint64_t tasks = stride >= chunk ? blocks * per_block : blocks / bpt;
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (uint64_t task = 0; task < tasks; task++) {
+      uint64_t w[MAXL], b[MAXL], o[MAXL] = {0};
+      uint64_t blk0 = task * bpt, off0 = 0, off1 = stride;
+      if (stride >= chunk) {
+        blk0 = task / per_block;
+        off0 = (task % per_block) * chunk;
+        off1 = off0 + chunk < stride ? off0 + chunk : stride;
+      }
+      for (uint64_t blk = blk0; blk < blk0 + bpt; blk++) {
+        const uint64_t start = blk * 2 * stride;
+        o[0] = off0;
+        if (off0)
+          mp_pow_mont(w, gap, o, &F);
+        else
+          mp_to_mont(w, one, &F);
+        for (uint64_t off = off0; off < off1; off++) {
+          uint64_t* pa = data + (start + off) * L;
+          uint64_t* pb = data + (start + off + stride) * L;
+          mp_montmul(b, w, pb, &F);
+          mp_submod(pb, pa, b, &F);
+          mp_addmod(pa, pa, b, &F);
+          mp_montmul(w, gap, w, &F);
+        }
+      }
+    }
+  }
+  if (inverse) {
+    uint64_t nn[MAXL] = {0}, nm[MAXL], two[MAXL] = {2}, pm2[MAXL];
+    nn[0] = n;
+    mp_to_mont(nm, nn, &F);
+    mp_sub(pm2, p, two, L);
+    mp_pow_mont(nm, nm, pm2, &F);
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (uint64_t i = 0; i < n; i++) mp_montmul(data + i * L, data + i * L, nm, &F);
+  }
+#pragma omp parallel for num_threads(threads) schedule(static)
+  for (uint64_t i = 0; i < n; i++) mp_from_mont(data + i * L, data + i * L, &F);
+  return 0;
+}
+
 /* Pointwise c = a*b mod p over n multi-precision elements (polymul oracle helper). */
 int oracle_mul_mp(uint64_t* c, const uint64_t* a, const uint64_t* b, uint64_t n, uint32_t limbs64,
                   const uint64_t* p) {

@@ -35,6 +35,9 @@ def load() -> C.CDLL:
         lib.oracle_ssip_u64.argtypes = [C.c_void_p, C.c_uint32, C.c_int64, C.c_int64]
         lib.oracle_ntt_mp.restype = C.c_int
         lib.oracle_ntt_mp.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_int]
+        lib.oracle_ntt_mp_par.restype = C.c_int
+        lib.oracle_ntt_mp_par.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_int,
+                                          C.c_int]
         lib.oracle_mul_mp.restype = C.c_int
         lib.oracle_mul_mp.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]
         _lib = lib
@@ -67,6 +70,17 @@ def ntt_mp(x: np.ndarray, p: int, g: int, inverse: bool = False) -> np.ndarray:
     n, L = d.shape
     pl, gl = _limbs(p, L), _limbs(g, L)  # keep the arrays alive across the call
     rc = load().oracle_ntt_mp(d.ctypes.data, n.bit_length() - 1, L, pl.ctypes.data, gl.ctypes.data, int(inverse))
+    assert rc == 0
+    return d
+
+
+def ntt_mp_par(x: np.ndarray, p: int, g: int, threads: int, inverse: bool = False) -> np.ndarray:
+    """ntt_mp with each stage split over `threads` OpenMP threads (bench.py's multi-core baseline)."""
+    d = np.ascontiguousarray(x, dtype=np.uint64).copy()
+    n, L = d.shape
+    pl, gl = _limbs(p, L), _limbs(g, L)
+    rc = load().oracle_ntt_mp_par(d.ctypes.data, n.bit_length() - 1, L, pl.ctypes.data, gl.ctypes.data,
+                                  int(inverse), int(threads))
     assert rc == 0
     return d
 

@@ -98,6 +98,17 @@ def main():
     b = pl.fill(pl.empty(), "random", seed=6)
     c = pl.empty()
     emit("2^24 inverse BN254 Fr", 1 << 24, timeit(lambda: pl.inverse(a)), passes=pl.passes)
+    # end-to-end window: host (pinned) -> HBM, forward, HBM -> host
+    h_in = a.cpu().pin_memory()
+    h_out = torch.empty_like(h_in).pin_memory()
+
+    def e2e():
+        c.copy_(h_in, non_blocking=True)
+        pl.forward(c)
+        h_out.copy_(c, non_blocking=True)
+    emit("2^24 forward BN254 Fr, end to end incl. H2D + D2H of 512 MiB each (pinned)", 1 << 24,
+         timeit(e2e, 5, 10))
+    del h_in, h_out
     emit("C5: polymul length 2^24 BN254 Fr (2 forward + pointwise + inverse), one GPU", 1 << 24,
          timeit(lambda: pl.polymul(a, b, c)))
     emit("coset forward 2^24 BN254 Fr (shift = generator 5)", 1 << 24, timeit(lambda: pl.forward_coset(a, 5)))
