@@ -50,6 +50,10 @@ template <int L, int W32>
 struct Eng29 {
   static constexpr int W = L;                   // registers per element
   static constexpr int MEMW = W32;              // 32-bit words per element in HBM (canonical)
+  // words per element of the plan's own scratch and outer-twiddle tables: 256-bit values (< 2p, p <
+  // 2^255) need 8 even in the 48-B caller layout, so only the first read and the last write of a
+  // transform move 48 B per element
+  static constexpr int SCRW = (L <= 9 && W32 > 8) ? 8 : W32;
   static constexpr int TW = (2 * L + 3) & ~3;   // words per twiddle-table entry: w, ws (16-B aligned)
   static constexpr int LDSW = L;                // words per element in LDS
   static constexpr int IN = 4;                  // DFT input bound (units of p)
@@ -86,15 +90,16 @@ struct Eng29 {
   // limb-wise; K = (value bound of b) + 1 keeps the top limb non-negative when p_top >= 3.
   enum : int { PC_5_29 = 0, PC_9_30 = 1, PC_4_29 = 2, PC_17_29 = 3, PC_7_30 = 4 };
 
+  template <int MW = W32>
   __device__ static __forceinline__ void load(uint32_t (&x)[W], const uint32_t* __restrict__ base, size_t idx) {
-    uint32_t w[W32];
-    const uint4* p = reinterpret_cast<const uint4*>(base + idx * W32);
+    uint32_t w[MW];
+    const uint4* p = reinterpret_cast<const uint4*>(base + idx * MW);
 #pragma unroll
-    for (int q = 0; q < W32 / 4; ++q) {
+    for (int q = 0; q < MW / 4; ++q) {
       const uint4 v = p[q];
       w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
     }
-    pack29<L, W32>(x, w);
+    pack29<L, MW>(x, w);
   }
   // x < FROM p (power of two) -> x < TO p by conditional subtractions of FROM/2 p, ..., TO p
   template <int FROM, int TO>
@@ -141,25 +146,26 @@ struct Eng29 {
     }
   }
   // x < BOUND p -> x < 2p (fits the HBM words: p < 2^255) -> HBM.  Between passes only.
-  template <int BOUND, bool FAST = false>
+  template <int BOUND, bool FAST = false, int MW = W32>
   __device__ static __forceinline__ void store_lazy(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
                                                     const Args& A) {
     reduce<BOUND, 2, FAST>(x, A);
-    put(base, idx, x);
+    put<MW>(base, idx, x);
   }
   // x < BOUND p -> canonical -> HBM
-  template <int BOUND, bool FAST = false>
+  template <int BOUND, bool FAST = false, int MW = W32>
   __device__ static __forceinline__ void store(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
                                                const Args& A) {
     reduce<BOUND, 1, FAST>(x, A);
-    put(base, idx, x);
+    put<MW>(base, idx, x);
   }
+  template <int MW = W32>
   __device__ static __forceinline__ void put(uint32_t* __restrict__ base, size_t idx, const uint32_t (&x)[W]) {
-    uint32_t w[W32];
-    unpack29<L, W32>(w, x);
-    uint4* p = reinterpret_cast<uint4*>(base + idx * W32);
+    uint32_t w[MW];
+    unpack29<L, MW>(w, x);
+    uint4* p = reinterpret_cast<uint4*>(base + idx * MW);
 #pragma unroll
-    for (int q = 0; q < W32 / 4; ++q) p[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    for (int q = 0; q < MW / 4; ++q) p[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
   }
   __device__ static __forceinline__ void tload(Tw& t, const uint32_t* __restrict__ tab, size_t idx) {
     const uint4* p = reinterpret_cast<const uint4*>(tab + idx * TW);
@@ -244,6 +250,7 @@ template <int N, int MEMW_>
 struct Eng32 {
   static constexpr int W = N;
   static constexpr int MEMW = MEMW_;
+  static constexpr int SCRW = MEMW_;
   static constexpr int TW = N;
   static constexpr int LDSW = N;
   static constexpr int IN = 4;
@@ -267,7 +274,9 @@ struct Eng32 {
     Tw w8[3];
     Tw ninv;
   };
+  template <int MW = MEMW_>
   __device__ static __forceinline__ void load(uint32_t (&x)[W], const uint32_t* __restrict__ base, size_t idx) {
+    static_assert(MW == MEMW_, "one HBM width");
     if constexpr (N == 1) {
       x[0] = reinterpret_cast<const uint2*>(base)[idx].x;
     } else {
@@ -282,14 +291,15 @@ struct Eng32 {
   static constexpr bool FASTRED = false;
   template <int FROM, int TO, bool FAST = false>
   __device__ static __forceinline__ void reduce(uint32_t (&)[W], const Args&) {}
-  template <int BOUND, bool FAST = false>
+  template <int BOUND, bool FAST = false, int MW = MEMW_>
   __device__ static __forceinline__ void store_lazy(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
                                                     const Args& A) {
-    store<BOUND>(base, idx, x, A);
+    store<BOUND, FAST, MW>(base, idx, x, A);
   }
-  template <int BOUND, bool FAST = false>
+  template <int BOUND, bool FAST = false, int MW = MEMW_>
   __device__ static __forceinline__ void store(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
                                                const Args&) {
+    static_assert(MW == MEMW_, "one HBM width");
     if constexpr (N == 1) {
       reinterpret_cast<uint2*>(base)[idx] = make_uint2(x[0], 0u);
     } else {

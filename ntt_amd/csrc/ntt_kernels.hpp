@@ -35,7 +35,8 @@ struct PassArgs {
   uint32_t mid_bits[4];  // final pass: middle digit widths, least significant (k_{p-1}) first
   uint32_t mid_off[4];   // final pass: output bit offset (relative to R_1) of those digits
   uint32_t flags;        // bit 0: multiply outputs by ninv (single-pass inverse)
-  size_t batch_stride;   // 32-bit words between batched transforms
+  uint32_t src_user;     // column pass: src is the caller's buffer (E::MEMW words/element), not scratch (E::SCRW)
+  size_t batch_stride;   // 32-bit words between batched transforms in the caller's buffers (n * E::MEMW)
 };
 
 template <class E, int KIND>

@@ -229,7 +229,7 @@ __device__ __forceinline__ void substage(uint32_t (&x)[E::EPT][E::W], uint32_t (
 //              A.tw_in over the in-column index d) and c^col folded into the outer-twiddle table
 //              (PlanImpl::coset).
 enum : int { PRO_NONE = 0, PRO_PW = 1, PRO_COSET = 2 };
-template <class E, int LOGR, int KIND, bool FULLTW, bool FAST, int PRO = PRO_NONE>
+template <class E, int LOGR, int KIND, bool FULLTW, bool FAST, int PRO = PRO_NONE, bool SRC_USER = true>
 __global__ __launch_bounds__((1 << E::TILE_LOG) / E::EPT) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
 void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                               const PassArgs<E> A) {
@@ -241,11 +241,18 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
   static_assert(LOGR >= QB && T >= 1, "radix");
   __shared__ __attribute__((aligned(16))) uint32_t lds[TE * LdsParts<E::LDSW, E::LDS_SPLIT>::max_words()];
 
+  // HBM words per element: the caller's buffers hold E::MEMW, the plan's scratch and outer-twiddle
+  // tables E::SCRW (8 for 256-bit values in the 48-B layout).  Column passes read the caller's
+  // buffer (pass 1, SRC_USER) or scratch and write scratch; the final pass reads scratch.
+  constexpr int SW = (KIND == KIND_COLUMN) ? (SRC_USER ? E::MEMW : E::SCRW) : (KIND == KIND_FINAL ? E::SCRW : E::MEMW);
+  constexpr int DW = (KIND == KIND_COLUMN) ? E::SCRW : E::MEMW;
+
   const int t = threadIdx.x;
   if (t >= NT) return;
-  const size_t boff = (size_t)blockIdx.y * A.batch_stride;
-  src += boff;
-  dst += boff;
+  const size_t bidx = (size_t)blockIdx.y * (A.batch_stride / E::MEMW);  // first element of this transform
+  src += bidx * SW;
+  dst += bidx * DW;
+  const size_t boff = bidx * E::MEMW;  // caller-buffer words (src2)
 
   // ------------------------------------------------------------------ workgroup geometry
   size_t colbase = 0;  // column pass: first element of this WG's column group
@@ -303,7 +310,7 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
         } else {
           pos = pi;
         }
-        E::load(x[j * Q + d], src, NTT_NOMEM(pos));
+        E::template load<SW>(x[j * Q + d], src, NTT_NOMEM(pos));
         if constexpr (PRO == PRO_PW) {
           uint32_t y[E::W];
           E::load(y, A.src2 + boff, pos);
@@ -358,7 +365,7 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
             // contiguous T * R run: HBM-streamed for pass 1, L2-resident later); the Montgomery
             // product removes R_e.  32 B per entry instead of a 80-B Shoup pair.
             uint32_t tw[E::W];
-            E::load(tw, A.tw_full, NTT_NOMEM(((size_t)col0 << LOGR) + (kn * T + c)));
+            E::template load<E::SCRW>(tw, A.tw_full, NTT_NOMEM(((size_t)col0 << LOGR) + (kn * T + c)));
             E::mulv(v, tw, A.F);
           } else {
             // outer twiddle w_{N_i}^{col * kn} = w_n^{(col * kn) << log_m} from the two-level
@@ -371,10 +378,10 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
             E::mulv(v, tl.w, A.F);
           }
           pos = colbase + c + ((size_t)kn << log_s);
-          E::template store_lazy<E::MUL_OUT, FAST>(dst, NTT_NOMEM(pos), v, A.F);  // scratch: < 2p, read by the next pass
+          E::template store_lazy<E::MUL_OUT, FAST, DW>(dst, NTT_NOMEM(pos), v, A.F);  // scratch: < 2p, read by the next pass
         } else if constexpr (KIND == KIND_FINAL) {
           pos = (size_t)(k10 + c) + ((size_t)midrev << A.r1) + ((size_t)kn << (A.log_n - LOGR));
-          E::template store<E::IN * Q, FAST>(dst, NTT_NOMEM(pos), v, A.F);
+          E::template store<E::IN * Q, FAST, DW>(dst, NTT_NOMEM(pos), v, A.F);
         } else {
           pos = kn;
           if (A.flags & 1u) {
@@ -443,7 +450,7 @@ __global__ void k_build_tw(uint32_t* __restrict__ out, size_t count, uint32_t lo
     E::mul(u.w, v, F);
     E::mulv(a.w, u.w, F);
   }
-  E::template store<E::MUL_OUT>(out, idx, a.w, F);
+  E::template store<E::MUL_OUT, false, E::SCRW>(out, idx, a.w, F);  // outer-twiddle tables: E::SCRW words
 }
 
 template <class E>
@@ -637,6 +644,21 @@ __global__ void k_pointwise_mul(const uint32_t* __restrict__ a, const uint32_t* 
 // ---------------------------------------------------------------------------- launchers
 // Radices the planner can emit: column/final passes use 3 <= r <= tile_log - MIN_COLS_LOG, single-workgroup
 // transforms 3 <= r <= tile_log.  Only those are instantiated.
+// Plain (no prologue) pass launch; later column passes of engines whose scratch is narrower than the
+// caller's layout read scratch (SRC_USER = false).
+template <class E, int LOGR, int KIND, bool FULLTW, bool FAST>
+static hipError_t launch_plain(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, dim3 g, dim3 b,
+                               hipStream_t st) {
+  if constexpr (KIND == KIND_COLUMN && E::SCRW != E::MEMW) {
+    if (!A.src_user) {
+      hipLaunchKernelGGL((k_pass<E, LOGR, KIND, FULLTW, FAST, PRO_NONE, false>), g, b, 0, st, src, dst, A);
+      return hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((k_pass<E, LOGR, KIND, FULLTW, FAST>), g, b, 0, st, src, dst, A);
+  return hipGetLastError();
+}
+
 template <class E, int KIND, int LOGR>
 static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t grid,
                                 uint32_t batch, hipStream_t st) {
@@ -659,25 +681,17 @@ static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassAr
             hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true, true, PRO_COSET>), g, b, 0, st, src, dst, A);
             return hipGetLastError();
           }
-          if (A.tw_full) {
-            hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true, true>), g, b, 0, st, src, dst, A);
-            return hipGetLastError();
-          }
+          if (A.tw_full) return launch_plain<E, LOGR, KIND, true, true>(src, dst, A, g, b, st);
         }
         if (A.src2 || A.tw_in) return hipErrorInvalidValue;  // fused prologues: FAST column + full tables
-        hipLaunchKernelGGL((k_pass<E, LOGR, KIND, false, true>), g, b, 0, st, src, dst, A);
-        return hipGetLastError();
+        return launch_plain<E, LOGR, KIND, false, true>(src, dst, A, g, b, st);
       }
     }
     if (A.src2 || A.tw_in) return hipErrorInvalidValue;
     if constexpr (KIND == KIND_COLUMN) {
-      if (A.tw_full) {
-        hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true, false>), g, b, 0, st, src, dst, A);
-        return hipGetLastError();
-      }
+      if (A.tw_full) return launch_plain<E, LOGR, KIND, true, false>(src, dst, A, g, b, st);
     }
-    hipLaunchKernelGGL((k_pass<E, LOGR, KIND, false, false>), g, b, 0, st, src, dst, A);
-    return hipGetLastError();
+    return launch_plain<E, LOGR, KIND, false, false>(src, dst, A, g, b, st);
   }
 }
 

@@ -277,6 +277,7 @@ struct PlanImpl final : PlanBase {
   static constexpr int NH = EngHost<E>::NH;
   static constexpr int TW = E::TW;
   static constexpr int MEMW = E::MEMW;
+  static constexpr int SCRW = E::SCRW;  // scratch and outer-twiddle tables (engines.hpp)
   HostField<NH> H;
   EngHost<E> EH;
   typename E::Args Ff{}, Fi{};
@@ -489,8 +490,8 @@ struct PlanImpl final : PlanBase {
     }
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return NTT_OK;
-    if (2 * elems * MEMW * 4 > free_b / 4) return NTT_OK;
-    if (hipMalloc(&d_full, 2 * elems * MEMW * 4) != hipSuccess) return NTT_ERR_HIP;
+    if (2 * elems * SCRW * 4 > free_b / 4) return NTT_OK;
+    if (hipMalloc(&d_full, 2 * elems * SCRW * 4) != hipSuccess) return NTT_ERR_HIP;
     for (int dir = 0; dir < 2; ++dir) {
       blk = log_n;
       for (unsigned i = 0; i + 1 < npass; ++i) {
@@ -498,7 +499,7 @@ struct PlanImpl final : PlanBase {
         const uint32_t* lo = d_tab + (dir ? off_los_i : off_los_f);
         const uint32_t* hi = d_tab + (dir ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
         // column-group-major layout of the pass kernel's tiles (T = TILE / R columns per workgroup)
-        if (launch_build_tw<E>(d_full + full_off[dir][i] * MEMW, 1ull << blk, r[i], tile_log_of<E>() - r[i],
+        if (launch_build_tw<E>(d_full + full_off[dir][i] * SCRW, 1ull << blk, r[i], tile_log_of<E>() - r[i],
                                log_n - blk, lo, hi, lo_bits, dir ? Fi : Ff, nullptr) != hipSuccess)
           return NTT_ERR_HIP;
         blk -= r[i];
@@ -598,7 +599,7 @@ struct PlanImpl final : PlanBase {
   // w_n^(col k) c^col R_e, layout of d_full (built on the device once per shift).
   int ensure_coset_full() {
     if (coset_full_ok) return NTT_OK;
-    if (!d_coset_full && hipMalloc(&d_coset_full, (size_t)n * MEMW * 4) != hipSuccess) {
+    if (!d_coset_full && hipMalloc(&d_coset_full, (size_t)n * SCRW * 4) != hipSuccess) {
       d_coset_full = nullptr;
       return NTT_ERR_HIP;
     }
@@ -625,7 +626,7 @@ struct PlanImpl final : PlanBase {
     if (d_scratch) hipFree(d_scratch);
     d_scratch = nullptr;
     scratch_elems = 0;
-    if (hipMalloc(&d_scratch, need * MEMW * 4) != hipSuccess) return NTT_ERR_HIP;
+    if (hipMalloc(&d_scratch, need * SCRW * 4) != hipSuccess) return NTT_ERR_HIP;
     scratch_elems = need;
     return NTT_OK;
   }
@@ -681,7 +682,7 @@ struct PlanImpl final : PlanBase {
         A.tw_hi = d_tab + (inverse ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
         // pass 1 of a memory-bound engine (8-B P path) computes its outer twiddles from the
         // L2-resident two-level tables: two 32-bit products are cheaper than streaming an n-entry table
-        A.tw_full = (use_full && (i > 0 || E::PASS1_FULL_TABLE)) ? d_full + full_off[inverse ? 1 : 0][i] * MEMW : nullptr;
+        A.tw_full = (use_full && (i > 0 || E::PASS1_FULL_TABLE)) ? d_full + full_off[inverse ? 1 : 0][i] * SCRW : nullptr;
         if (i == 0 && in2) {
           A.src2 = in2;
           A.tw_full = d_full_pm;
@@ -692,6 +693,7 @@ struct PlanImpl final : PlanBase {
         }
         A.log_blk = blk;
         A.log_m = log_n - blk;
+        A.src_user = (i == 0) ? 1u : 0u;
         const uint32_t* src = (i == 0) ? in : d_scratch;
         e = launch_pass<E>(KIND_COLUMN, (int)r[i], src, d_scratch, A, grid, batch, st);
         mark(st);
@@ -729,7 +731,7 @@ struct PlanImpl final : PlanBase {
   int ensure_polymul_table() {
     if (d_full_pm) return NTT_OK;
     const size_t elems = 1ull << log_n;
-    if (hipMalloc(&d_full_pm, elems * MEMW * 4) != hipSuccess) {
+    if (hipMalloc(&d_full_pm, elems * SCRW * 4) != hipSuccess) {
       d_full_pm = nullptr;
       return NTT_ERR_HIP;
     }

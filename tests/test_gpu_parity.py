@@ -246,8 +246,9 @@ def test_custom_modulus_matches_builtin():
     assert torch.equal(ta, tb)
 
 
-def test_batch_forward():
-    fid, L, log_n, batch = 1, 4, 12, 3
+@pytest.mark.parametrize("fid,L,log_n,batch", [(1, 4, 12, 3), (2, 6, 12, 3), (1, 6, 17, 2), (0, 1, 15, 3)])
+def test_batch_forward(fid, L, log_n, batch):
+    """Batched transforms (the 48-B layout with 17 = 6+6+5 also runs a scratch-to-scratch pass)."""
     pl = _plan(fid, log_n, L)
     t = pl.empty(batch)
     x = np.concatenate([OC.random_limbs(fid, 1 << log_n, seed=s, L=L) for s in range(batch)])
@@ -257,6 +258,8 @@ def test_batch_forward():
     n = 1 << log_n
     for s in range(batch):
         assert np.array_equal(got[s * n:(s + 1) * n], _oracle_forward(x[s * n:(s + 1) * n], fid, L))
+    pl.inverse_batch(t, batch)
+    assert np.array_equal(_host(t, L), x)
 
 
 def _is_prime(n: int) -> bool:
