@@ -61,7 +61,6 @@ def cpu_ntt(x: Sequence[int], p: int, g: int) -> List[int]:
     n = len(x)
     L = n.bit_length() - 1
     a = [v % p for v in x]
-    half = n >> 1
     m = n
     while m > 1:
         h = m >> 1
@@ -78,10 +77,9 @@ def cpu_ntt(x: Sequence[int], p: int, g: int) -> List[int]:
     for i in range(n):
         r = int(format(i, f"0{L}b")[::-1], 2) if L else 0
         out[r] = a[i]
-    del half
     return out
 
 
-def cpu_ntt_c1(log_n: int = 12, seed: int = 1) -> List[int]:
+def cpu_ntt_c1(log_n: int = 12) -> List[int]:
     """Config C1: 2^12 forward NTT over BN254 Fr of x_j = j on the CPU."""
     return cpu_ntt(list(range(1 << log_n)), BN254_FR, 5)
