@@ -63,3 +63,19 @@ def test_plan_create_reports_no_device_or_bad_args_without_gpu():
     st = so.ntt_plan_create(C.byref(h), 1, 10, 4, 0)
     assert st in (-5, -2)  # no device
     assert so.ntt_plan_create(C.byref(h), 7, 10, 4, 0) == -1  # bad field id
+
+
+def test_mplan_create_fails_cleanly_without_gpu_or_bad_args():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("CPU-only check")
+    from ntt_amd import lib as L
+    so = L.load()
+    h = C.c_void_p()
+    devs = (C.c_int * 3)(0, 1, 2)
+    assert so.ntt_mplan_create(C.byref(h), 1, 16, 4, 3, devs) == -1  # not a power of two
+    assert so.ntt_mplan_create(C.byref(h), 1, 2, 4, 8, devs) == -1   # 2^2 cannot split over 8
+    st = so.ntt_mplan_create(C.byref(h), 1, 16, 4, 1, devs)
+    assert st in (-5, -2, -1) and not h.value
+    assert so.ntt_forward_multi(None, None, None) == -1
+    assert so.ntt_mplan_destroy(None) == 0
