@@ -316,3 +316,24 @@ def test_384bit_class_large_modulus_against_c_oracle(bits):
         assert np.array_equal(_host(t, 6), OC.ntt_mp(x, p, g, False)), (bits, log_n)
         pl.inverse(t)
         assert np.array_equal(_host(t, 6), x), (bits, log_n)
+
+
+def test_max_size_2pow28_bn254_kat_and_round_trip():
+    """BN254 Fr at 2^28 (its largest single-GPU BASELINE size, C4's n): the KAT of x_j = j at sampled k
+    and the inverse round trip, checked on the device (8 GiB vector, 4 passes)."""
+    fid, L, log_n = 1, 4, 28
+    p, g = R.FIELDS[fid]
+    n = 1 << log_n
+    pl = _plan(fid, log_n, L)
+    t = pl.empty()
+    pl.fill(t, "iota")
+    pl.forward(t)
+    rng = np.random.default_rng(28)
+    ks = [0, 1, 2, 3, n // 2, n - 1] + [int(k) for k in rng.integers(0, n, 24)]
+    rows = t[torch.tensor(ks, device=t.device)].cpu().numpy().view(np.uint64)
+    for k, row in zip(ks, rows):
+        v = sum(int(row[i]) << (64 * i) for i in range(L))
+        assert v == R.kat_xj(n, p, g, k), k
+    pl.inverse(t)
+    iota = torch.arange(n, dtype=torch.int64, device=t.device)
+    assert torch.equal(t[:, 0], iota) and not bool(t[:, 1:].any())
