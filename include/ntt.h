@@ -97,6 +97,12 @@ int ntt_pointwise_mul(ntt_plan* plan, const void* d_a, const void* d_b, void* d_
  * inverse's first pass).  a and b are overwritten with their transforms; c may alias a or b. */
 int ntt_polymul(ntt_plan* plan, void* d_a, void* d_b, void* d_c, void* hip_stream);
 
+/* Canonical-range check of a caller buffer (the contract every transform assumes: elements < p,
+ * upper limbs zero).  The reference's only guard is CGBN's padded-store `BAD LIMB` trap
+ * (impl_cuda.cu:1402-1408); this is a query instead: *bad = number of the `count` elements that are
+ * not < p.  Blocking on hip_stream. */
+int ntt_count_noncanonical(ntt_plan* plan, const void* d_data, uint64_t count, uint64_t* bad, void* hip_stream);
+
 /* Fill a device vector with the SURVEY §8d synthetic inputs: kind 0 = x_j = j (the reference's
  * input, GZKP-NTT.cu:1587), kind 1 = SplitMix64 limbs with the top limb masked (seeded). */
 int ntt_fill(ntt_plan* plan, void* d_data, int kind, uint64_t seed, void* hip_stream);

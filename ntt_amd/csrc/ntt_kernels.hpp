@@ -17,6 +17,15 @@ using Eng384 = Eng29<14, 12>;  // 6 x 64-bit limbs in HBM, moduli up to 2^383
 using Eng256w = Eng29<9, 12>;  // 6 x 64-bit limbs in HBM, moduli < 2^255 (256-bit arithmetic)
 using EngP = Eng32<1, 2>;      // P469762049, `long long` in HBM
 
+// a modulus as W little-endian 32-bit words (canonical-range checks)
+template <int W>
+struct ModWords {
+  uint32_t w[W];
+};
+template <class E>
+hipError_t launch_count_noncanonical(const uint32_t* d, size_t n, const ModWords<E::MEMW>& p,
+                                     unsigned long long* bad, hipStream_t st);
+
 template <class E>
 struct PassArgs {
   typename E::Args F;

@@ -641,6 +641,31 @@ __global__ void k_pointwise_mul(const uint32_t* __restrict__ a, const uint32_t* 
   E::template store<E::MUL_OUT>(c, j, x, F);
 }
 
+// Canonical-range check (the reference's padded-store `BAD LIMB` trap, impl_cuda.cu:1402-1408, as a
+// query): counts elements that are not < p in a caller buffer of E::MEMW-word elements.  p holds
+// the modulus in MEMW little-endian 32-bit words (zero above its top word).
+template <int MEMW>
+__global__ void k_count_noncanonical(const uint32_t* __restrict__ d, size_t n, ModWords<MEMW> p,
+                                     unsigned long long* __restrict__ bad) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* e = d + i * MEMW;
+  int cmp = 0;  // sign of e - p, decided by the most significant differing word
+#pragma unroll
+  for (int k = MEMW - 1; k >= 0; --k)
+    if (cmp == 0 && e[k] != p.w[k]) cmp = e[k] < p.w[k] ? -1 : 1;
+  if (cmp >= 0) atomicAdd(bad, 1ull);
+}
+
+template <class E>
+hipError_t launch_count_noncanonical(const uint32_t* d, size_t n, const ModWords<E::MEMW>& p,
+                                     unsigned long long* bad, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL((k_count_noncanonical<E::MEMW>), dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, d, n, p,
+                     bad);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------- launchers
 // Radices the planner can emit: column/final passes use 3 <= r <= tile_log - MIN_COLS_LOG, single-workgroup
 // transforms 3 <= r <= tile_log.  Only those are instantiated.
@@ -776,6 +801,8 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
                                          const uint32_t*, uint32_t, const typename E::Args&, hipStream_t,          \
                                          const uint32_t*, const uint32_t*);                                        \
   template hipError_t launch_scale_pow<E>(uint32_t*, uint32_t, uint32_t, const uint32_t*, const uint32_t*, uint32_t, \
-                                          const typename E::Args&, hipStream_t);
+                                          const typename E::Args&, hipStream_t);                                   \
+  template hipError_t launch_count_noncanonical<E>(const uint32_t*, size_t, const ModWords<E::MEMW>&,              \
+                                                   unsigned long long*, hipStream_t);
 
 }  // namespace ntt

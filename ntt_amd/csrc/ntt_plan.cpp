@@ -90,6 +90,7 @@ struct PlanBase {
                            uint64_t row0, bool inverse, hipStream_t st) = 0;
   virtual int transpose(const void* src, void* dst, unsigned log_rows, unsigned log_cols, hipStream_t st) = 0;
   virtual int coset(void* d, const uint64_t* shift, unsigned limbs64, bool inverse, hipStream_t st) = 0;
+  virtual int count_noncanonical(const void* d, uint64_t count, uint64_t* bad, hipStream_t st) = 0;
   uint64_t n = 0;
   unsigned flags = 0;
   unsigned log_n = 0, elem_bytes = 0, npass = 0;
@@ -305,6 +306,7 @@ struct PlanImpl final : PlanBase {
     if (d_scratch) hipFree(d_scratch);
     if (d_full) hipFree(d_full);
     if (d_full_pm) hipFree(d_full_pm);
+    if (d_bad) hipFree(d_bad);
     if (d_coset) hipFree(d_coset);
     if (d_coset_full) hipFree(d_coset_full);
     for (auto& row : ev)
@@ -536,6 +538,25 @@ struct PlanImpl final : PlanBase {
   bool coset_full_ok = false;
   size_t coset_off[2][3] = {};  // [dir][lo_s, hi, u^d (forward only)] word offsets into d_coset
   std::vector<uint32_t> pm2_;    // p - 2 (inversion exponent)
+
+  unsigned long long* d_bad = nullptr;  // canonical-range check counter
+  int count_noncanonical(const void* d, uint64_t count, uint64_t* bad, hipStream_t st) override {
+    if (!d || !bad) return NTT_ERR_ARG;
+    if (!d_bad && hipMalloc(&d_bad, sizeof(*d_bad)) != hipSuccess) {
+      d_bad = nullptr;
+      return NTT_ERR_HIP;
+    }
+    ModWords<MEMW> pw{};
+    for (int i = 0; i < NH && i < MEMW; ++i) pw.w[i] = H.M.p[i];
+    unsigned long long h = 0;
+    if (hipMemsetAsync(d_bad, 0, sizeof(*d_bad), st) != hipSuccess ||
+        launch_count_noncanonical<E>(static_cast<const uint32_t*>(d), count, pw, d_bad, st) != hipSuccess ||
+        hipMemcpyAsync(&h, d_bad, sizeof(h), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return NTT_ERR_HIP;
+    *bad = h;
+    return NTT_OK;
+  }
 
   int coset(void* d, const uint64_t* shift, unsigned limbs64, bool inverse, hipStream_t st) override {
     if (!d || !shift || (flags & NTT_PLAN_TWIDDLE_ONLY)) return NTT_ERR_ARG;
@@ -920,6 +941,16 @@ int ntt_inverse_coset(ntt_plan* plan, void* d, const uint64_t* shift, void* s) {
 int ntt_pointwise_mul(ntt_plan* plan, const void* a, const void* b, void* c, void* s) {
   if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
   return set_err(plan->impl->pointwise(a, b, c, static_cast<hipStream_t>(s)));
+}
+
+int ntt_count_noncanonical(ntt_plan* plan, const void* d, uint64_t count, uint64_t* bad, void* s) {
+  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
+  int cur = 0;
+  hipGetDevice(&cur);
+  if (cur != plan->impl->device) hipSetDevice(plan->impl->device);
+  const int rc = plan->impl->count_noncanonical(d, count, bad, static_cast<hipStream_t>(s));
+  if (cur != plan->impl->device) hipSetDevice(cur);
+  return set_err(rc);
 }
 
 int ntt_polymul(ntt_plan* plan, void* a, void* b, void* c, void* s) {

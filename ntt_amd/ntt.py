@@ -137,6 +137,16 @@ class NTTPlan:
                  "ntt_inverse")
         return t
 
+    def count_noncanonical(self, t: torch.Tensor, stream=None) -> int:
+        """Number of elements of t that are not < p (the transforms' input contract); blocking."""
+        if t.device.type != "cuda" or not t.is_contiguous() or t.dtype != torch.int64:
+            raise ValueError("expected a contiguous int64 device tensor in the element layout")
+        count = t.numel() if self.limbs64 == 1 else t.numel() // self.limbs64
+        bad = C.c_uint64()
+        _L.check(self._lib.ntt_count_noncanonical(self._h, C.c_void_p(t.data_ptr()), count, C.byref(bad),
+                                                  _stream_ptr(stream, t.device)), "ntt_count_noncanonical")
+        return bad.value
+
     def forward_batch(self, t: torch.Tensor, batch: int, stream=None) -> torch.Tensor:
         self._check_tensor(t, batch)
         _L.check(self._lib.ntt_forward_batch(self._h, C.c_void_p(t.data_ptr()), int(batch),

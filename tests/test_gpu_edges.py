@@ -96,3 +96,18 @@ def test_adversarial_near_p_against_oracle(fid, L):
         got = _run(_plan(fid, log_n, L), x)
         exp = OC.ntt_mp(x, p, g, False)
         assert np.array_equal(got, exp), (fid, L, log_n)
+
+
+@pytest.mark.parametrize("fid,L", [(1, 4), (2, 6), (0, 1), (0, 4)])
+def test_count_noncanonical(fid, L):
+    """ntt_count_noncanonical: synthetic inputs are canonical; p, p + 1 and all-ones limbs are not,
+    p - 1 is."""
+    from ntt_amd.ntt import NTTPlan, to_device
+    p, _ = R.FIELDS[fid]
+    pl = NTTPlan(fid, 12, L)
+    t = pl.fill(pl.empty(), "random", seed=3)
+    assert pl.count_noncanonical(t) == 0
+    bad = to_device([p, p + 1, (1 << (64 * L - 1)) - 1, p - 1], L)
+    t[5:9] = bad
+    t[20] = -1  # all limbs 0xffff...: not a residue in any layout
+    assert pl.count_noncanonical(t) == 4
