@@ -101,7 +101,21 @@ def cpu_baseline(field_id: int, limbs: int, log_n: int):
                       f"os.cpu_count()={os.cpu_count()}, affinity {avail}): {dtp:.2f} s",
             "seconds": dtp,
             "single_core": {"value": (1 << log_n) / dt1, "cores": 1, "seconds": dt1,
-                            "sample": f"one 2^{log_n}-point forward NTT, scalar C oracle, 1 core"}}
+                            "sample": f"one 2^{log_n}-point forward NTT, scalar C oracle, 1 core"},
+            "reference_field_single_core": _cpu_reference_field()}
+
+
+def _cpu_reference_field(log_n: int = 22):
+    """The reference's own CPU path on its own field: GZKP-NTT.cu:30-48 (DIT + bit reversal over
+    P = 469762049, 64-bit arithmetic) as restated by oracle_ntt_u64, 1 core, x_j = j (its input)."""
+    import numpy as np
+    from oracle import oracle_c as OC
+    x = np.arange(1 << log_n, dtype=np.int64)
+    t0 = time.perf_counter()
+    OC.ntt_u64(x, 469762049, 3)
+    dt = time.perf_counter() - t0
+    return {"value": (1 << log_n) / dt, "unit": "field-elements/s", "cores": 1, "seconds": dt,
+            "sample": f"one 2^{log_n}-point forward NTT over P469762049 (the reference's CPU NTT, restated)"}
 
 
 def load_traffic(tag: str):
