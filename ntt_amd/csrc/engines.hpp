@@ -19,6 +19,9 @@
 #ifndef NTT_EPT_256
 #define NTT_EPT_256 4
 #endif
+#ifndef NTT_256_PASS1_TABLE
+#define NTT_256_PASS1_TABLE 1
+#endif
 #ifndef NTT_P_SCRATCH32
 #define NTT_P_SCRATCH32 1
 #endif
@@ -71,7 +74,7 @@ struct Eng29 {
   static constexpr int WAVES_PER_EU = (L <= 9) ? (EPT == 4 ? NTT_WAVES_256 : 2) : 2;
   static constexpr bool LDS_SPLIT = false;
   static constexpr int MIN_COLS_LOG = 2;  // column passes own >= 4 adjacent columns: >= 128-B runs
-  static constexpr bool PASS1_FULL_TABLE = true;  // VALU-bound: a table read beats a second product
+  static constexpr bool PASS1_FULL_TABLE = NTT_256_PASS1_TABLE;  // VALU-bound: a table read beats a second product
   // quotient-estimate reduction needs p's top limb >= 2^18: possible only when 29L - 18 <= 255
   static constexpr bool FASTRED = 29 * L - 18 <= 255;
   struct Tw {
