@@ -337,3 +337,22 @@ def test_max_size_2pow28_bn254_kat_and_round_trip():
     pl.inverse(t)
     iota = torch.arange(n, dtype=torch.int64, device=t.device)
     assert torch.equal(t[:, 0], iota) and not bool(t[:, 1:].any())
+
+
+@pytest.mark.parametrize("log_n", [20, 21, 22, 23, 24, 25])
+def test_p_path_every_large_size_kat_and_round_trip(log_n):
+    """The 8-B SSIP path at every large size (its schedules differ per size: narrow-first radices,
+    4-B scratch): closed-form KAT of x_j = j at sampled k and the inverse round trip."""
+    p, g = R.FIELDS[0]
+    n = 1 << log_n
+    pl = _plan(0, log_n, 1)
+    t = pl.empty()
+    pl.fill(t, "iota")
+    pl.forward(t)
+    rng = np.random.default_rng(log_n)
+    ks = [0, 1, 2, n // 2, n - 1] + [int(k) for k in rng.integers(0, n, 16)]
+    got = t[torch.tensor(ks, device=t.device)].cpu().tolist()
+    for k, v in zip(ks, got):
+        assert v == R.kat_xj(n, p, g, k), (log_n, k, pl.passes)
+    pl.inverse(t)
+    assert torch.equal(t, torch.arange(n, dtype=torch.int64, device=t.device))
