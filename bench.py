@@ -7,17 +7,23 @@ A "step" is one forward transform of a whole 2^24-element vector (SURVEY §8d sy
 SplitMix64 limbs), resident in HBM when the timed region starts.
 
 * N = 1: one MI355X, one 2^24 transform per step.
-* N > 1 (torch.distributed.run, one rank per GPU): a 2^24 transform fits one GPU, and the
-  north star partitions the transform only from 2^26 up.  So every rank transforms its own 2^24
-  polynomial (different seeds), there is no data-path collective, and `value` = N * 2^24 / t with
-  t = max over ranks ("scaling": "weak").
-* --four-step: ONE transform of 2^log_n split over the N ranks with the RCCL all-to-all
-  (SURVEY §8e, strong scaling; e.g. BASELINE config 4: --four-step --log-n 28 on 8 GPUs).
+* N > 1 (torch.distributed.run, one rank per GPU): by default ONE 2^24 transform split over the N
+  ranks as the four-step with the RCCL all-to-all ("scaling": "strong"; `value` =
+  2^24 / t, t = max over ranks).  ``--independent`` instead runs one 2^24 transform per rank with no
+  data-path collective ("weak", `value` = N 2^24 / t): a secondary line, linear by construction.
+* ``--four-step`` at N = 1 times the partitioned schedule on one GPU (RCCL world size 1);
+  ``--log-n 28 --four-step`` on 8 GPUs is BASELINE config 4.
 
-Rank 0 prints one JSON line with `roofline` (HBM roofline of the dominant kernel, measured with
-HIP events on its launch stream inside the timed region), `valu_roofline` (the same launch against
-the v_mad_u64_u32 issue peak: the kernels are bound by 256-bit multiply-adds, not by HBM; see
-DESIGN.md §7) and `cpu_baseline` (the C oracle on the host, a bounded sample).
+Rank 0 prints one JSON line with
+* `roofline`: SURVEY §8(d)'s transform-level HBM roofline — algorithmic bytes 2·n·S per forward
+  (one read + one write of the vector) ÷ time per transform ÷ (G × 8 TB/s); `traffic` = the
+  rocprofv3 PMC HBM bytes of one transform (FETCH_SIZE ×2 + WRITE_SIZE, MI355X_MICROARCH.md
+  gfx950 correction) when the committed summary was measured on these kernel sources, else null.
+  `roofline.dominant_kernel` = the same for the longest launch alone (HIP events on its stream
+  inside the timed region);
+* `valu_roofline`: that launch against the v_mad_u64_u32 issue peak (the kernels are bound by
+  256-bit multiply-adds, DESIGN.md §7);
+* `cpu_baseline`: the C oracle on the host (a bounded sample; see cpu_baseline()).
 """
 from __future__ import annotations
 
@@ -67,15 +73,27 @@ def parse():
     ap.add_argument("--inverse", action="store_true", help="time the inverse instead of the forward")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--four-step", "--dist", dest="four_step", action="store_true",
-                    help="one transform split over all ranks (four-step + RCCL all-to-all)")
-    ap.add_argument("--cpu-log-n", type=int, default=22, help="C-oracle sample size (log2)")
+                    help="one transform split over all ranks (four-step + RCCL all-to-all); default for N > 1")
+    ap.add_argument("--independent", action="store_true",
+                    help="N > 1: one independent transform per rank (weak scaling, no data-path collective)")
+    ap.add_argument("--cpu-log-n", type=int, default=22, help="C-oracle single-core sample size (log2)")
     return ap.parse_args()
+
+
+def _cpu_share():
+    """Threads the C oracle may use: the harness's per-GPU CPU share (OMP_NUM_THREADS, 16 on the GPU
+    boxes, whose os.cpu_count() counts the whole 256-thread machine) or the affinity mask."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        avail = os.cpu_count() or 1
+    return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail, avail
 
 
 def cpu_baseline(field_id: int, limbs: int, log_n: int):
     """The C oracle (oracle/ntt_oracle.c, a restatement of GZKP-NTT.cu:30-48) on the host: the full
-    2^24 workload split over the box's CPU share (OpenMP, OMP_NUM_THREADS or <= 16 threads, the
-    multiprocess leg of SURVEY §8d), plus a bounded 1-core sample of the scalar restatement."""
+    2^24 workload split over the box's CPU share (OpenMP, the multiprocess leg of SURVEY §8d), plus a
+    bounded 1-core sample of the scalar restatement and the reference's own CPU NTT on its own field."""
     from oracle import oracle_c as OC
     from oracle import ntt_ref as R
     p, g = R.FIELDS[field_id]
@@ -84,11 +102,7 @@ def cpu_baseline(field_id: int, limbs: int, log_n: int):
     OC.ntt_mp(x, p, g)
     dt1 = time.perf_counter() - t0
     del x
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except AttributeError:  # pragma: no cover
-        avail = os.cpu_count() or 1
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, avail)
+    threads, avail = _cpu_share()
     big = 24
     xb = OC.random_limbs(field_id, 1 << big, seed=2, L=limbs)
     t0 = time.perf_counter()
@@ -97,8 +111,9 @@ def cpu_baseline(field_id: int, limbs: int, log_n: int):
     cpu = platform.processor() or platform.machine()
     return {"value": (1 << big) / dtp, "unit": "field-elements/s", "cores": threads, "kind": "port",
             "sample": f"one 2^{big}-point forward NTT ({FIELD_NAMES[field_id]}, {limbs}x64-bit limbs, SplitMix64 "
-                      f"input) by the C oracle split over {threads} OpenMP threads ({cpu}, "
-                      f"os.cpu_count()={os.cpu_count()}, affinity {avail}): {dtp:.2f} s",
+                      f"input) by the C oracle split over {threads} OpenMP threads ({cpu}): {dtp:.2f} s",
+            "cores_note": f"{threads} threads = this process's CPU share (OMP_NUM_THREADS / affinity {avail}); "
+                          f"os.cpu_count()={os.cpu_count()} counts the whole host, which one GPU's job may not use",
             "seconds": dtp,
             "single_core": {"value": (1 << log_n) / dt1, "cores": 1, "seconds": dt1,
                             "sample": f"one 2^{log_n}-point forward NTT, scalar C oracle, 1 core"},
@@ -106,26 +121,39 @@ def cpu_baseline(field_id: int, limbs: int, log_n: int):
 
 
 def _cpu_reference_field(log_n: int = 22):
-    """The reference's own CPU path on its own field: GZKP-NTT.cu:30-48 (DIT + bit reversal over
-    P = 469762049, 64-bit arithmetic) as restated by oracle_ntt_u64, 1 core, x_j = j (its input)."""
+    """The reference's own CPU path on its own field, P = 469762049, x_j = j (its input), 1 core:
+    GZKP-NTT.cu:30-48 itself (oracle/_ref, compiled from the reference sources; kind "reference")
+    when built, else its restatement oracle_ntt_u64 (kind "port")."""
     import numpy as np
     from oracle import oracle_c as OC
+    from oracle import ref_c
     x = np.arange(1 << log_n, dtype=np.int64)
+    if ref_c.available():
+        kind, fn = "reference", (lambda v: ref_c.ntt(v))
+    else:
+        kind, fn = "port", (lambda v: OC.ntt_u64(v, 469762049, 3))
     t0 = time.perf_counter()
-    OC.ntt_u64(x, 469762049, 3)
+    fn(x)
     dt = time.perf_counter() - t0
-    return {"value": (1 << log_n) / dt, "unit": "field-elements/s", "cores": 1, "seconds": dt,
-            "sample": f"one 2^{log_n}-point forward NTT over P469762049 (the reference's CPU NTT, restated)"}
+    return {"value": (1 << log_n) / dt, "unit": "field-elements/s", "cores": 1, "seconds": dt, "kind": kind,
+            "sample": f"one 2^{log_n}-point forward NTT over P469762049 (GZKP-NTT.cu NTT, "
+                      f"{'the reference code itself' if kind == 'reference' else 'restated'})"}
 
 
 def load_traffic(tag: str):
-    """HBM bytes per launch from the committed rocprofv3 --pmc summary for this workload (or None)."""
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary (tools/pmc_to_traffic.py) for
+    this workload, only if it was measured on the current kernel sources; else (None, reason)."""
+    from ntt_amd.build import source_hash
     path = os.path.join(HERE, "profiles", "pmc_summary.json")
     try:
-        d = json.load(open(path))
-        return d.get(tag)
+        ent = json.load(open(path)).get(tag)
     except Exception:
-        return None
+        return None, "no profiles/pmc_summary.json"
+    if not isinstance(ent, dict):
+        return None, f"no PMC summary for {tag}"
+    if ent.get("src_hash") != source_hash():
+        return None, f"stale: PMC summary measured on sources {ent.get('src_hash')}, current {source_hash()}"
+    return ent.get("launch_bytes"), ent.get("profile")
 
 
 def main():
@@ -138,22 +166,25 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.independent and args.four_step:
+        raise SystemExit("--independent and --four-step are exclusive")
+    four_step = args.four_step or (world > 1 and not args.independent)
     # one rank per GPU; the modulo only matters when rehearsing several ranks on one device
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     n = 1 << args.log_n
 
-    use_dist = world > 1 or args.four_step
+    use_dist = world > 1 or four_step
     if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29512")
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
-        if args.four_step:  # the data path exchanges over RCCL (all-to-all)
+        if four_step:  # the data path exchanges over RCCL (all-to-all)
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:  # independent transforms: the only collectives are the timing barrier and max
             dist.init_process_group("gloo")
-    if args.four_step:
+    if four_step:
         from ntt_amd.distributed import DistNTT
         eng = DistNTT(field_id=args.field, log_n=args.log_n, limbs64=args.limbs, device=local)
         data = eng.empty()
@@ -192,20 +223,20 @@ def main():
 
     elapsed = t1 - t0
     if use_dist:
-        dev = f"cuda:{local}" if args.four_step else "cpu"
+        dev = f"cuda:{local}" if four_step else "cpu"
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms_per_step = elapsed / args.steps * 1e3
-    jobs = 1 if args.four_step else world  # independent 2^log_n transforms per step
+    jobs = 1 if four_step else world  # independent 2^log_n transforms per step
     value = jobs * n / (elapsed / args.steps)
 
     elem_bytes = 8 if args.limbs == 1 else 8 * args.limbs
     passes = list(getattr(plan_for_prof, "passes", []))
+    what = "inverse" if args.inverse else "forward"
     out = {
         "metric": METRIC if (args.field == 1 and args.log_n == 24 and not args.inverse) else
-        f"field-elements/sec, 2^{args.log_n} {'inverse' if args.inverse else 'forward'} NTT over "
-        f"{FIELD_NAMES[args.field]}",
+        f"field-elements/sec, 2^{args.log_n} {what} NTT over {FIELD_NAMES[args.field]}",
         "value": value,
         "unit": "field-elements/s",
         "n_gpus": world,
@@ -213,39 +244,51 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "strong" if args.four_step else "weak",
+        "scaling": "strong" if four_step else "weak",
         "vs_baseline": None,
         "dtype": ("u256 mod p: 9 x 29-bit limbs, u32 x u32 + u64 MAD (v_mad_u64_u32)" if args.limbs == 4 else
                   ("u384 mod p: 14 x 29-bit limbs, u32 x u32 + u64 MAD" if args.limbs == 6 else
                    "u32 mod p (Montgomery)")),
         "data": "synthetic: SplitMix64 field elements (SURVEY §8d vector B, seed 2), resident in HBM",
-        "config": {"workload": f"2^{args.log_n}-point {'inverse' if args.inverse else 'forward'} NTT, "
+        "config": {"workload": f"2^{args.log_n}-point {what} NTT, "
                                f"{FIELD_NAMES[args.field]}, {args.limbs}x64-bit limbs, natural order, in place",
                    "log_n": args.log_n, "field": FIELD_NAMES[args.field], "limbs64": args.limbs,
                    "passes_log_radix": passes,
-                   "parallelism": (f"four-step over {world} GPU(s) (RCCL all-to-all)" if args.four_step else
-                                   ("single GPU" if world == 1 else
-                                    f"{world} GPUs, one independent transform per rank (no data-path collective)")),
+                   "parallelism": (f"four-step over {world} GPU(s) (RCCL all-to-all, one transform)" if four_step
+                                   else ("single GPU" if world == 1 else
+                                         f"{world} GPUs, one independent transform per rank (no data-path "
+                                         f"collective)")),
                    "transforms_per_step": jobs},
     }
+    # ---- SURVEY §8(d) roofline of the whole transform: 2 n S algorithmic bytes per transform
+    gpus_per_transform = world if four_step else 1
+    alg_transform = 2 * n * elem_bytes
+    t_transform = ms_per_step * 1e-3 * (1 if four_step else 1)  # every rank runs its transform(s) per step
+    achieved = alg_transform / t_transform / gpus_per_transform / 1e9
+    tag = f"f{args.field}_L{args.limbs}_n{args.log_n}_w{gpus_per_transform}{'_inv' if args.inverse else ''}"
+    launch_bytes, prof_src = load_traffic(tag) if not four_step else (None, "four-step: not profiled")
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS,
+            "traffic": (sum(launch_bytes) / gpus_per_transform if launch_bytes else None),
+            "traffic_source": prof_src,
+            "algorithmic_bytes": alg_transform / gpus_per_transform,
+            "definition": "SURVEY §8(d): 2·n·S bytes per transform (one read + one write of the vector) "
+                          "÷ time per transform ÷ (G × 8 TB/s); traffic = PMC HBM bytes per transform per GPU"}
     if launch_avg:
-        # dominant kernel = the longest launch; algorithmic bytes per launch = one read + one write
-        # of the local vector (2*n*S per pass over all n elements).
+        # dominant kernel = the longest launch; algorithmic bytes per launch = one read + one write of
+        # the vector it sweeps (the local share in four-step mode)
         k = max(range(len(launch_avg)), key=lambda i: launch_avg[i])
-        local_n = n // world if args.four_step else n
+        local_n = n // world if four_step else n
         alg_bytes = 2 * local_n * elem_bytes
-        achieved = alg_bytes / (launch_avg[k] * 1e-3) / 1e9
-        tag = f"f{args.field}_L{args.limbs}_n{args.log_n}_w{world if args.four_step else 1}"
-        traffic = load_traffic(tag)
-        out["roofline"] = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                           "frac": achieved / HBM_PEAK_GBPS,
-                           "traffic": traffic[k] if isinstance(traffic, list) and k < len(traffic) else None,
-                           "kernel": f"launch {k} of {len(launch_avg)}", "kernel_ms": launch_avg[k],
-                           "algorithmic_bytes_per_launch": alg_bytes,
-                           "launch_ms": launch_avg}
-        total_alg = 2 * local_n * elem_bytes * max(1, len(launch_avg))
-        out["hbm_effective_gbps_per_gpu"] = total_alg / (ms_per_step * 1e-3) / 1e9
-        if args.limbs == 4 and args.field in (1, 2) and not args.four_step and len(passes) == len(launch_avg) \
+        ach_k = alg_bytes / (launch_avg[k] * 1e-3) / 1e9
+        roof["dominant_kernel"] = {"kernel": f"launch {k} of {len(launch_avg)}", "kernel_ms": launch_avg[k],
+                                   "achieved": ach_k, "frac": ach_k / HBM_PEAK_GBPS,
+                                   "algorithmic_bytes_per_launch": alg_bytes,
+                                   "traffic": (launch_bytes[k] if launch_bytes and k < len(launch_bytes) else None)}
+        roof["launch_ms"] = launch_avg
+        if launch_bytes and len(launch_bytes) == len(launch_avg):
+            out["hbm_pmc_gbps_per_gpu"] = sum(launch_bytes) / (sum(launch_avg) * 1e-3) / 1e9
+        if args.limbs == 4 and args.field in (1, 2) and not four_step and len(passes) == len(launch_avg) \
                 and len(passes) >= 2:
             # compute roofline of the same launch: MADs issued per launch / its duration vs the
             # v_mad_u64_u32 issue peak (the binding resource)
@@ -254,6 +297,7 @@ def main():
             out["valu_roofline"] = {"bound": "valu (v_mad_u64_u32 issue)", "achieved": ach, "peak": MAD_PEAK_T,
                                     "unit": "T lane-MAD/s", "frac": ach / MAD_PEAK_T,
                                     "mads_per_launch": mads, "kernel": f"launch {k} of {len(launch_avg)}"}
+    out["roofline"] = roof
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args.field, args.limbs if args.limbs != 1 else 1, args.cpu_log_n)

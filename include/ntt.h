@@ -22,7 +22,8 @@
  *     status (0 ok, < 0 error, see ntt_strerror), prints nothing, and the plan API is asynchronous
  *     on the given hipStream_t (NULL = default stream).  The reference-shaped shims SSIP /
  *     NTT_GZKP_256 keep the reference's blocking behaviour.
- *   - plans are thread-compatible: one plan per thread, or serialise calls on a plan.
+ *   - plans are thread-compatible: one plan per thread, or serialise calls on a plan.  The status
+ *     of the last call (ntt_last_error) is kept per thread; the shims' plan cache is locked.
  */
 #ifndef NTT_AMD_NTT_H
 #define NTT_AMD_NTT_H
@@ -96,6 +97,12 @@ int ntt_pointwise_mul(ntt_plan* plan, const void* d_a, const void* d_b, void* d_
  * of their pointwise product into c (multi-pass 256-bit plans fuse the pointwise product into the
  * inverse's first pass).  a and b are overwritten with their transforms; c may alias a or b. */
 int ntt_polymul(ntt_plan* plan, void* d_a, void* d_b, void* d_c, void* hip_stream);
+/* Second half of a polymul over `batch` transforms laid out back to back: c = INTT(a * b) for a, b
+ * already forward-transformed (fused into the inverse's first pass where the plan allows it).
+ * c may alias a or b; a may equal b (squaring).  The distributed polymul runs it on each rank's
+ * column-layout shares (ntt_polymul_multi, ntt_amd/distributed.py). */
+int ntt_inverse_pointwise_batch(ntt_plan* plan, const void* d_a, const void* d_b, void* d_c, unsigned batch,
+                                void* hip_stream);
 
 /* Canonical-range check of a caller buffer (the contract every transform assumes: elements < p,
  * upper limbs zero).  The reference's only guard is CGBN's padded-store `BAD LIMB` trap
@@ -123,6 +130,14 @@ int ntt_twiddle_pack(ntt_plan* plan, const void* d_src, void* d_dst, unsigned lo
                      unsigned log_block, uint64_t row0, int inverse, void* hip_stream);
 int ntt_transpose(ntt_plan* plan, const void* d_src, void* d_dst, unsigned log_rows, unsigned log_cols,
                   void* hip_stream);
+/* The same with explicit chunk strides (several vectors exchanged in one all-to-all, e.g. the
+ * distributed polymul's a and b): twiddle_pack writes peer chunk q at dst + q * peer_stride
+ * elements (peer_stride >= 2^(log_rows + log_block)); transpose reads source rows in blocks of
+ * 2^log_block_rows rows, block q starting at src + q * block_stride elements. */
+int ntt_twiddle_pack_ex(ntt_plan* plan, const void* d_src, void* d_dst, unsigned log_rows, unsigned log_row_len,
+                        unsigned log_block, uint64_t row0, int inverse, uint64_t peer_stride, void* hip_stream);
+int ntt_transpose_ex(ntt_plan* plan, const void* d_src, void* d_dst, unsigned log_rows, unsigned log_cols,
+                     unsigned log_block_rows, uint64_t block_stride, void* hip_stream);
 
 /* Per-launch timing for benchmarks: when enabled, every transform records HIP events on its
  * stream between its kernel launches (a ring of 64 transforms, no host synchronisation);
@@ -165,6 +180,13 @@ typedef struct ntt_mplan ntt_mplan;
 int ntt_mplan_create(ntt_mplan** out, int field_id, unsigned log_n, unsigned limbs64, int ngpus, const int* devices);
 int ntt_forward_multi(ntt_mplan* plan, void* const* d_data, void* const* hip_streams);
 int ntt_inverse_multi(ntt_mplan* plan, void* const* d_data, void* const* hip_streams);
+/* Distributed cyclic polynomial product (BASELINE config 5): d_a[g], d_b[g] hold the
+ * row-layout shares of a and b; on return d_c[g] holds the row-layout share of c = a * b (length n)
+ * and d_a / d_b hold the column-layout shares of their forward transforms.  Forward(a) and
+ * forward(b) share ONE all-to-all (each peer chunk carries both), the pointwise product is local
+ * and fused into the inverse's first column pass, and the inverse's all-to-all brings c back to
+ * the row layout: two exchanges for the three transforms.  d_c may alias d_a or d_b. */
+int ntt_polymul_multi(ntt_mplan* plan, void* const* d_a, void* const* d_b, void* const* d_c, void* const* hip_streams);
 /* each device's row-layout share of the global synthetic vector (kinds as ntt_fill) */
 int ntt_mplan_fill(ntt_mplan* plan, void* const* d_data, int kind, uint64_t seed, void* const* hip_streams);
 int ntt_mplan_info(const ntt_mplan* plan, uint64_t* local_n, unsigned* log_n1, unsigned* log_n2);

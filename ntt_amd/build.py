@@ -28,6 +28,20 @@ SOURCES += ["ntt_plan.cpp", "ntt_multi.cpp"]
 ARCH = os.environ.get("NTT_OFFLOAD_ARCH", "gfx950")
 
 
+def source_hash() -> str:
+    """16-hex digest of every kernel / C-ABI source and header: tags measurements (PMC traffic in
+    profiles/pmc_summary.json) with the code they were taken on, so bench.py never reports stale bytes."""
+    import hashlib
+    h = hashlib.sha256()
+    for d in (CSRC, INCLUDE):
+        for f in sorted(os.listdir(d)):
+            if f.endswith((".hip", ".hpp", ".cpp", ".h")):
+                h.update(f.encode())
+                with open(os.path.join(d, f), "rb") as fh:
+                    h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def hipcc() -> str:
     for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
         if cand and os.path.exists(cand):

@@ -68,9 +68,10 @@ hipError_t launch_fill(int kind, uint32_t* dst, size_t n, uint64_t seed, uint32_
 template <class E>
 hipError_t launch_twiddle_pack(const uint32_t* src, uint32_t* dst, uint32_t log_rows, uint32_t log_len,
                                uint32_t log_bw, uint64_t row0, uint32_t log_n, const uint32_t* lo, const uint32_t* hi,
-                               uint32_t lo_bits, const typename E::Args& F, hipStream_t st);
+                               uint32_t lo_bits, const typename E::Args& F, uint64_t peer_stride, hipStream_t st);
 template <class E>
-hipError_t launch_transpose(const uint32_t* src, uint32_t* dst, uint32_t log_rows, uint32_t log_cols, hipStream_t st);
+hipError_t launch_transpose(const uint32_t* src, uint32_t* dst, uint32_t log_rows, uint32_t log_cols,
+                            uint32_t log_blk_rows, uint64_t blk_stride, hipStream_t st);
 // data[j] *= c^j (coset / low-degree-extension scale), c^j = lo_s[j & mask] * hi[j >> lo_bits]
 template <class E>
 hipError_t launch_scale_pow(uint32_t* data, uint32_t log_n, uint32_t batch, const uint32_t* lo_s, const uint32_t* hi,

@@ -465,14 +465,15 @@ hipError_t launch_build_tw(uint32_t* out, size_t count, uint32_t log_r, uint32_t
 // ---------------------------------------------------------------------------- four-step helpers
 // Multi-GPU four-step, local steps.  twiddle_pack: src is [rows][row_len] (row-major);
 // element (a, b) is multiplied by w_n^((row0 + a) * b) and written to dst block b / bw (bw =
-// row_len / G) at a * bw + b % bw, i.e. dst = [G][rows][bw]: one contiguous chunk per peer for the
-// all-to-all.  Twiddles from the plan's two-level tables: lo_s holds lo * R_e (R_e the engine's
+// row_len / G) at blk * peer_stride + a * bw + b % bw, i.e. dst = [G][rows][bw] (peer_stride =
+// rows * bw): one contiguous chunk per peer for the all-to-all.  A larger peer_stride interleaves
+// several vectors' chunks per peer (the distributed polymul exchanges a and b in one all-to-all).  Twiddles from the plan's two-level tables: lo_s holds lo * R_e (R_e the engine's
 // Montgomery radix), so t = lo_s[e & mask] * hi[e >> lo_bits] = w_n^e R_e and mulv(x, t) = x w_n^e.
 template <class E>
 __global__ void k_twiddle_pack(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t log_rows,
                                uint32_t log_len, uint32_t log_bw, uint64_t row0, uint32_t log_n,
                                const uint32_t* __restrict__ lo, const uint32_t* __restrict__ hi, uint32_t lo_bits,
-                               const typename E::Args F) {
+                               const typename E::Args F, uint64_t peer_stride) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (1ull << (log_rows + log_len))) return;
   const uint64_t a = i >> log_len, b = i & ((1ull << log_len) - 1);
@@ -485,7 +486,7 @@ __global__ void k_twiddle_pack(const uint32_t* __restrict__ src, uint32_t* __res
   E::mul(w.w, h, F);
   E::mulv(x, w.w, F);
   const size_t blk = b >> log_bw, off = b & ((1ull << log_bw) - 1);
-  E::template store<E::MUL_OUT>(dst, (blk << (log_rows + log_bw)) + (a << log_bw) + off, x, F);
+  E::template store<E::MUL_OUT>(dst, blk * peer_stride + (a << log_bw) + off, x, F);
 }
 
 // Coset scale (low-degree-extension step): data[j] *= c^j over `batch` vectors of 2^log_n elements,
@@ -518,11 +519,15 @@ hipError_t launch_scale_pow(uint32_t* data, uint32_t log_n, uint32_t batch, cons
   return hipGetLastError();
 }
 
-// dst[c][r] = src[r][c] for a rows x cols matrix of MEMW-word elements (32x32 tiles through LDS).
+// dst[c][r] = src[r][c] for a rows x cols matrix of MEMW-word elements (32x32 tiles through LDS,
+// 16-B vector accesses).  Source rows come in blocks of 2^log_blk_rows rows, block b starting at
+// element b * blk_stride (blk_stride = 2^(log_blk_rows + log_cols): one dense matrix; larger: the
+// per-peer chunks of an all-to-all that carried several vectors).
 template <int MEMW>
 __global__ void k_transpose(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t log_rows,
-                            uint32_t log_cols) {
+                            uint32_t log_cols, uint32_t log_blk_rows, uint64_t blk_stride) {
   constexpr int TILE = 32;
+  constexpr bool VEC = (MEMW % 4) == 0;
   __shared__ uint32_t tile[TILE][TILE + 1][MEMW];
   const uint64_t rows = 1ull << log_rows, cols = 1ull << log_cols;
   const uint64_t bx = (uint64_t)blockIdx.x * TILE, by = (uint64_t)blockIdx.y * TILE;
@@ -530,9 +535,21 @@ __global__ void k_transpose(const uint32_t* __restrict__ src, uint32_t* __restri
   for (int k = ty; k < TILE; k += 8) {
     const uint64_t r = by + k, c = bx + tx;
     if (r < rows && c < cols) {
-      const uint32_t* s = src + (r * cols + c) * MEMW;
+      const uint64_t rin = r & ((1ull << log_blk_rows) - 1);
+      const uint32_t* s = src + ((r >> log_blk_rows) * blk_stride + (rin << log_cols) + c) * MEMW;
+      if constexpr (VEC) {
 #pragma unroll
-      for (int w = 0; w < MEMW; ++w) tile[k][tx][w] = s[w];
+        for (int w = 0; w < MEMW / 4; ++w) {
+          const uint4 v = reinterpret_cast<const uint4*>(s)[w];
+          tile[k][tx][4 * w] = v.x;
+          tile[k][tx][4 * w + 1] = v.y;
+          tile[k][tx][4 * w + 2] = v.z;
+          tile[k][tx][4 * w + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int w = 0; w < MEMW; ++w) tile[k][tx][w] = s[w];
+      }
     }
   }
   __syncthreads();
@@ -540,8 +557,15 @@ __global__ void k_transpose(const uint32_t* __restrict__ src, uint32_t* __restri
     const uint64_t c = bx + k, r = by + tx;
     if (r < rows && c < cols) {
       uint32_t* d = dst + (c * rows + r) * MEMW;
+      if constexpr (VEC) {
 #pragma unroll
-      for (int w = 0; w < MEMW; ++w) d[w] = tile[tx][k][w];
+        for (int w = 0; w < MEMW / 4; ++w)
+          reinterpret_cast<uint4*>(d)[w] =
+              make_uint4(tile[tx][k][4 * w], tile[tx][k][4 * w + 1], tile[tx][k][4 * w + 2], tile[tx][k][4 * w + 3]);
+      } else {
+#pragma unroll
+        for (int w = 0; w < MEMW; ++w) d[w] = tile[tx][k][w];
+      }
     }
   }
 }
@@ -549,18 +573,20 @@ __global__ void k_transpose(const uint32_t* __restrict__ src, uint32_t* __restri
 template <class E>
 hipError_t launch_twiddle_pack(const uint32_t* src, uint32_t* dst, uint32_t log_rows, uint32_t log_len,
                                uint32_t log_bw, uint64_t row0, uint32_t log_n, const uint32_t* lo, const uint32_t* hi,
-                               uint32_t lo_bits, const typename E::Args& F, hipStream_t st) {
+                               uint32_t lo_bits, const typename E::Args& F, uint64_t peer_stride, hipStream_t st) {
   const size_t total = 1ull << (log_rows + log_len);
   hipLaunchKernelGGL((k_twiddle_pack<E>), dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, st, src, dst, log_rows,
-                     log_len, log_bw, row0, log_n, lo, hi, lo_bits, F);
+                     log_len, log_bw, row0, log_n, lo, hi, lo_bits, F, peer_stride);
   return hipGetLastError();
 }
 
 template <class E>
-hipError_t launch_transpose(const uint32_t* src, uint32_t* dst, uint32_t log_rows, uint32_t log_cols, hipStream_t st) {
+hipError_t launch_transpose(const uint32_t* src, uint32_t* dst, uint32_t log_rows, uint32_t log_cols,
+                            uint32_t log_blk_rows, uint64_t blk_stride, hipStream_t st) {
   const uint64_t rows = 1ull << log_rows, cols = 1ull << log_cols;
   const dim3 grid((uint32_t)((cols + 31) / 32), (uint32_t)((rows + 31) / 32));
-  hipLaunchKernelGGL((k_transpose<E::MEMW>), grid, dim3(256), 0, st, src, dst, log_rows, log_cols);
+  hipLaunchKernelGGL((k_transpose<E::MEMW>), grid, dim3(256), 0, st, src, dst, log_rows, log_cols, log_blk_rows,
+                     blk_stride);
   return hipGetLastError();
 }
 
@@ -793,8 +819,9 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
                                      uint32_t, hipStream_t);                                                       \
   template hipError_t launch_twiddle_pack<E>(const uint32_t*, uint32_t*, uint32_t, uint32_t, uint32_t, uint64_t,   \
                                              uint32_t, const uint32_t*, const uint32_t*, uint32_t,                 \
-                                             const typename E::Args&, hipStream_t);                                \
-  template hipError_t launch_transpose<E>(const uint32_t*, uint32_t*, uint32_t, uint32_t, hipStream_t);           \
+                                             const typename E::Args&, uint64_t, hipStream_t);                      \
+  template hipError_t launch_transpose<E>(const uint32_t*, uint32_t*, uint32_t, uint32_t, uint32_t, uint64_t,     \
+                                          hipStream_t);                                                            \
   template hipError_t launch_pointwise<E>(const uint32_t*, const uint32_t*, uint32_t*, size_t,                     \
                                           const typename E::Args&, const uint32_t*, hipStream_t);                  \
   template hipError_t launch_build_tw<E>(uint32_t*, size_t, uint32_t, uint32_t, uint32_t, const uint32_t*,        \

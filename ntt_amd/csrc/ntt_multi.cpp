@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstdlib>
 #include <vector>
 
 #include "ntt.h"
@@ -28,14 +29,20 @@ struct Rccl {
   ncclResult_t (*AllToAll)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*GroupStart)() = nullptr;
   ncclResult_t (*GroupEnd)() = nullptr;
-  bool ok() const { return CommInitAll && CommDestroy && AllToAll && GroupStart && GroupEnd; }
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  bool ok() const { return CommInitAll && CommDestroy && AllToAll && GroupStart && GroupEnd && Send && Recv; }
 };
 
 const Rccl& rccl() {
   static const Rccl r = [] {
     Rccl x;
     void* h = RTLD_DEFAULT;
-    if (!dlsym(h, "ncclCommInitAll")) {
+    // NTT_RCCL_LIBRARY: an explicit RCCL (or a fault-injecting stand-in, tests/test_gpu_mplan_faults.py)
+    if (const char* lib = getenv("NTT_RCCL_LIBRARY"); lib && *lib) {
+      h = dlopen(lib, RTLD_NOW | RTLD_LOCAL);
+      if (!h) return x;
+    } else if (!dlsym(h, "ncclCommInitAll")) {
       h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
       if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
       if (!h) return x;
@@ -45,6 +52,8 @@ const Rccl& rccl() {
     x.AllToAll = reinterpret_cast<decltype(x.AllToAll)>(dlsym(h, "ncclAllToAll"));
     x.GroupStart = reinterpret_cast<decltype(x.GroupStart)>(dlsym(h, "ncclGroupStart"));
     x.GroupEnd = reinterpret_cast<decltype(x.GroupEnd)>(dlsym(h, "ncclGroupEnd"));
+    x.Send = reinterpret_cast<decltype(x.Send)>(dlsym(h, "ncclSend"));
+    x.Recv = reinterpret_cast<decltype(x.Recv)>(dlsym(h, "ncclRecv"));
     return x;
   }();
   return r;
@@ -59,6 +68,7 @@ struct ntt_mplan {
   std::vector<int> dev;
   std::vector<ntt_plan*> rows, cols, tw;
   std::vector<void*> send, recv;
+  std::vector<void*> send2, recv2;  // 2 local_n each: the polymul's batched (a, b) exchange, on first use
   std::vector<ncclComm_t> comm;
 
   ~ntt_mplan() {
@@ -69,6 +79,8 @@ struct ntt_mplan {
       if (g < comm.size() && comm[g]) rccl().CommDestroy(comm[g]);
       if (g < send.size() && send[g]) hipFree(send[g]);
       if (g < recv.size() && recv[g]) hipFree(recv[g]);
+      if (g < send2.size() && send2[g]) hipFree(send2[g]);
+      if (g < recv2.size() && recv2[g]) hipFree(recv2[g]);
       if (g < cols.size() && cols[g] && cols[g] != rows[g]) ntt_plan_destroy(cols[g]);
       if (g < rows.size() && rows[g]) ntt_plan_destroy(rows[g]);
       if (g < tw.size() && tw[g]) ntt_plan_destroy(tw[g]);
@@ -89,19 +101,134 @@ struct DeviceGuard {
   ~DeviceGuard() { hipSetDevice(cur); }
 };
 
-int exchange(ntt_mplan* m, void* const* streams) {
-  // per-peer chunk: r * c elements, moved as 64-bit words
-  const size_t words = (1ull << (m->log_r + m->log_c)) * (m->elem_bytes / 8);
+// RCCL moves at most 2^31 - 1 bytes per peer per collective (a 2 GiB per-peer chunk arrived half
+// copied with ncclAllToAll: 2^26 BN254 on one device, tests/test_gpu_fullsize.py), so per-peer chunks
+// above kMaxPeerBytes are exchanged as grouped ncclSend/ncclRecv pieces instead.
+constexpr size_t kMaxPeerBytes = size_t(1) << 30;
+
+// All-to-all of per-peer chunks of `words` 64-bit words: send[g] = [G][words] -> recv[g] = [G][words].
+int exchange(ntt_mplan* m, const std::vector<void*>& send, const std::vector<void*>& recv, size_t words,
+             void* const* streams) {
   const Rccl& R = rccl();
   if (R.GroupStart() != ncclSuccess) return NTT_ERR_RCCL;
-  for (int g = 0; g < m->ngpus; ++g) {
-    hipSetDevice(m->dev[g]);
-    if (R.AllToAll(m->send[g], m->recv[g], words, ncclUint64, m->comm[g], m->stream(streams, g)) != ncclSuccess) {
-      R.GroupEnd();
-      return NTT_ERR_RCCL;
+  ncclResult_t st = ncclSuccess;
+  if (words * 8 <= kMaxPeerBytes) {
+    for (int g = 0; g < m->ngpus && st == ncclSuccess; ++g) {
+      hipSetDevice(m->dev[g]);
+      st = R.AllToAll(send[g], recv[g], words, ncclUint64, m->comm[g], m->stream(streams, g));
+    }
+  } else {
+    const size_t piece = kMaxPeerBytes / 8;
+    for (int g = 0; g < m->ngpus && st == ncclSuccess; ++g) {
+      hipSetDevice(m->dev[g]);
+      hipStream_t s = m->stream(streams, g);
+      auto* sb = static_cast<uint64_t*>(send[g]);
+      auto* rb = static_cast<uint64_t*>(recv[g]);
+      for (int h = 0; h < m->ngpus && st == ncclSuccess; ++h)
+        for (size_t off = 0; off < words && st == ncclSuccess; off += piece) {
+          const size_t cnt = words - off < piece ? words - off : piece;
+          st = R.Send(sb + h * words + off, cnt, ncclUint64, h, m->comm[g], s);
+          if (st == ncclSuccess) st = R.Recv(rb + h * words + off, cnt, ncclUint64, h, m->comm[g], s);
+        }
     }
   }
-  return R.GroupEnd() == ncclSuccess ? NTT_OK : NTT_ERR_RCCL;
+  // always close the group: the calls already issued for other devices are launched (or dropped) by
+  // RCCL as a unit, never left pending in the thread's group state
+  const ncclResult_t end = R.GroupEnd();
+  return (st == ncclSuccess && end == ncclSuccess) ? NTT_OK : NTT_ERR_RCCL;
+}
+
+size_t chunk_words(const ntt_mplan* m) {  // per-peer chunk of one vector: r * c elements
+  return (1ull << (m->log_r + m->log_c)) * (m->elem_bytes / 8);
+}
+
+// After a failed step the other devices may still hold queued work that reads or writes the
+// caller's buffers: wait for every device's stream before reporting the error, so the caller can
+// free or reuse them.
+int drain(ntt_mplan* m, void* const* streams, int rc) {
+  for (int g = 0; g < m->ngpus; ++g) {
+    hipSetDevice(m->dev[g]);
+    hipStreamSynchronize(m->stream(streams, g));
+  }
+  return rc;
+}
+
+int ensure_pair_buffers(ntt_mplan* m) {
+  if (m->send2.empty()) {
+    m->send2.assign(m->ngpus, nullptr);
+    m->recv2.assign(m->ngpus, nullptr);
+  }
+  for (int g = 0; g < m->ngpus; ++g) {
+    if (m->send2[g]) continue;
+    hipSetDevice(m->dev[g]);
+    if (hipMalloc(&m->send2[g], 2 * m->local_n() * m->elem_bytes) != hipSuccess) {
+      m->send2[g] = nullptr;
+      return NTT_ERR_HIP;
+    }
+    if (hipMalloc(&m->recv2[g], 2 * m->local_n() * m->elem_bytes) != hipSuccess) {
+      hipFree(m->send2[g]);
+      m->send2[g] = nullptr;
+      return NTT_ERR_HIP;
+    }
+  }
+  return NTT_OK;
+}
+
+// Forward of several vectors in row layout to column layout with ONE exchange: v[k][g] is vector k's
+// share on device g; the per-peer chunks of all vectors travel together ([G][nv][chunk]).
+int forward_vectors(ntt_mplan* m, void* const* const* v, int nv, void* const* streams) {
+  const uint64_t r = 1ull << m->log_r, chunk = 1ull << (m->log_r + m->log_c);
+  const std::vector<void*>& sb = nv == 1 ? m->send : m->send2;
+  const std::vector<void*>& rb = nv == 1 ? m->recv : m->recv2;
+  for (int g = 0; g < m->ngpus; ++g) {
+    hipSetDevice(m->dev[g]);
+    void* s = m->stream(streams, g);
+    for (int k = 0; k < nv; ++k) {
+      if (int rc = ntt_forward_batch(m->rows[g], v[k][g], (unsigned)r, s)) return rc;
+      if (int rc = ntt_twiddle_pack_ex(m->tw[g], v[k][g], static_cast<char*>(sb[g]) + k * chunk * m->elem_bytes,
+                                       m->log_r, m->log_n2, m->log_c, (uint64_t)g * r, 0, nv * chunk, s))
+        return rc;
+    }
+  }
+  if (int rc = exchange(m, sb, rb, nv * chunk_words(m), streams)) return rc;
+  for (int g = 0; g < m->ngpus; ++g) {
+    hipSetDevice(m->dev[g]);
+    void* s = m->stream(streams, g);
+    for (int k = 0; k < nv; ++k) {
+      // recv = [G][nv][r][c]: vector k's rows g' r .. (g'+1) r - 1 at (g' nv + k) chunk -> [c][n1]
+      if (int rc = ntt_transpose_ex(m->tw[g], static_cast<const char*>(rb[g]) + k * chunk * m->elem_bytes, v[k][g],
+                                    m->log_n1, m->log_c, m->log_r, nv * chunk, s))
+        return rc;
+      if (int rc = ntt_forward_batch(m->cols[g], v[k][g], 1u << m->log_c, s)) return rc;
+    }
+  }
+  return NTT_OK;
+}
+
+// Inverse from column layout to row layout.  With `b` (polymul) the first column pass starts from
+// the pointwise product a * b (ntt_inverse_pointwise_batch) and the result lands in `out`.
+int inverse_vector(ntt_mplan* m, void* const* a, void* const* b, void* const* out, void* const* streams) {
+  const uint64_t c = 1ull << m->log_c;
+  for (int g = 0; g < m->ngpus; ++g) {
+    hipSetDevice(m->dev[g]);
+    void* s = m->stream(streams, g);
+    if (b) {
+      if (int rc = ntt_inverse_pointwise_batch(m->cols[g], a[g], b[g], out[g], (unsigned)c, s)) return rc;
+    } else if (int rc = ntt_inverse_batch(m->cols[g], out[g], (unsigned)c, s)) {
+      return rc;
+    }
+    if (int rc = ntt_twiddle_pack(m->tw[g], out[g], m->send[g], m->log_c, m->log_n1, m->log_r, (uint64_t)g * c, 1, s))
+      return rc;
+  }
+  if (int rc = exchange(m, m->send, m->recv, chunk_words(m), streams)) return rc;
+  for (int g = 0; g < m->ngpus; ++g) {
+    hipSetDevice(m->dev[g]);
+    void* s = m->stream(streams, g);
+    // recv = [G][c][r] = [n2][r] -> [r][n2]
+    if (int rc = ntt_transpose(m->tw[g], m->recv[g], out[g], m->log_n2, m->log_r, s)) return rc;
+    if (int rc = ntt_inverse_batch(m->rows[g], out[g], 1u << m->log_r, s)) return rc;
+  }
+  return NTT_OK;
 }
 
 }  // namespace
@@ -155,47 +282,28 @@ int ntt_mplan_create(ntt_mplan** out, int field_id, unsigned log_n, unsigned lim
 int ntt_forward_multi(ntt_mplan* m, void* const* d_data, void* const* streams) {
   if (!m || !d_data) return NTT_ERR_ARG;
   DeviceGuard guard;
-  const uint64_t r = 1ull << m->log_r;
-  for (int g = 0; g < m->ngpus; ++g) {
-    hipSetDevice(m->dev[g]);
-    void* s = m->stream(streams, g);
-    if (int rc = ntt_forward_batch(m->rows[g], d_data[g], (unsigned)r, s)) return rc;
-    if (int rc = ntt_twiddle_pack(m->tw[g], d_data[g], m->send[g], m->log_r, m->log_n2, m->log_c, (uint64_t)g * r,
-                                  0, s))
-      return rc;
-  }
-  if (int rc = exchange(m, streams)) return rc;
-  for (int g = 0; g < m->ngpus; ++g) {
-    hipSetDevice(m->dev[g]);
-    void* s = m->stream(streams, g);
-    // recv = [G][r][c] = [n1][c] -> [c][n1]
-    if (int rc = ntt_transpose(m->tw[g], m->recv[g], d_data[g], m->log_n1, m->log_c, s)) return rc;
-    if (int rc = ntt_forward_batch(m->cols[g], d_data[g], 1u << m->log_c, s)) return rc;
-  }
-  return NTT_OK;
+  void* const* v[1] = {d_data};
+  const int rc = forward_vectors(m, v, 1, streams);
+  return rc ? drain(m, streams, rc) : NTT_OK;
 }
 
 int ntt_inverse_multi(ntt_mplan* m, void* const* d_data, void* const* streams) {
   if (!m || !d_data) return NTT_ERR_ARG;
   DeviceGuard guard;
-  const uint64_t c = 1ull << m->log_c;
-  for (int g = 0; g < m->ngpus; ++g) {
-    hipSetDevice(m->dev[g]);
-    void* s = m->stream(streams, g);
-    if (int rc = ntt_inverse_batch(m->cols[g], d_data[g], (unsigned)c, s)) return rc;
-    if (int rc = ntt_twiddle_pack(m->tw[g], d_data[g], m->send[g], m->log_c, m->log_n1, m->log_r, (uint64_t)g * c,
-                                  1, s))
-      return rc;
-  }
-  if (int rc = exchange(m, streams)) return rc;
-  for (int g = 0; g < m->ngpus; ++g) {
-    hipSetDevice(m->dev[g]);
-    void* s = m->stream(streams, g);
-    // recv = [G][c][r] = [n2][r] -> [r][n2]
-    if (int rc = ntt_transpose(m->tw[g], m->recv[g], d_data[g], m->log_n2, m->log_r, s)) return rc;
-    if (int rc = ntt_inverse_batch(m->rows[g], d_data[g], 1u << m->log_r, s)) return rc;
-  }
-  return NTT_OK;
+  const int rc = inverse_vector(m, nullptr, nullptr, d_data, streams);
+  return rc ? drain(m, streams, rc) : NTT_OK;
+}
+
+int ntt_polymul_multi(ntt_mplan* m, void* const* d_a, void* const* d_b, void* const* d_c, void* const* streams) {
+  if (!m || !d_a || !d_b || !d_c) return NTT_ERR_ARG;
+  DeviceGuard guard;
+  if (int rc = ensure_pair_buffers(m)) return rc;
+  bool same = true;  // squaring: a == b on every device -> one forward transform
+  for (int g = 0; g < m->ngpus; ++g) same = same && d_a[g] == d_b[g];
+  void* const* v[2] = {d_a, d_b};
+  int rc = same ? forward_vectors(m, v, 1, streams) : forward_vectors(m, v, 2, streams);
+  if (rc == NTT_OK) rc = inverse_vector(m, d_a, d_b, d_c, streams);
+  return rc ? drain(m, streams, rc) : NTT_OK;
 }
 
 int ntt_mplan_fill(ntt_mplan* m, void* const* d_data, int kind, uint64_t seed, void* const* streams) {

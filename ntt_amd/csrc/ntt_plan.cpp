@@ -87,8 +87,10 @@ struct PlanBase {
   virtual int fill(void* d, uint64_t count, int kind, uint64_t seed, uint64_t row0, unsigned log_inner,
                    unsigned log_stride, hipStream_t st) = 0;
   virtual int twiddle_pack(const void* src, void* dst, unsigned log_rows, unsigned log_len, unsigned log_bw,
-                           uint64_t row0, bool inverse, hipStream_t st) = 0;
-  virtual int transpose(const void* src, void* dst, unsigned log_rows, unsigned log_cols, hipStream_t st) = 0;
+                           uint64_t row0, bool inverse, uint64_t peer_stride, hipStream_t st) = 0;
+  virtual int transpose(const void* src, void* dst, unsigned log_rows, unsigned log_cols, unsigned log_blk_rows,
+                        uint64_t blk_stride, hipStream_t st) = 0;
+  virtual int inverse_pointwise(const void* a, const void* b, void* c, unsigned batch, hipStream_t st) = 0;
   virtual int coset(void* d, const uint64_t* shift, unsigned limbs64, bool inverse, hipStream_t st) = 0;
   virtual int count_noncanonical(const void* d, uint64_t count, uint64_t* bad, hipStream_t st) = 0;
   uint64_t n = 0;
@@ -768,23 +770,37 @@ struct PlanImpl final : PlanBase {
   // multiplies at load (one HBM pass and one kernel fewer than forward / pointwise / inverse).
   int polymul(void* a, void* b, void* c, hipStream_t st) override {
     if (!a || !b || !c || (flags & NTT_PLAN_TWIDDLE_ONLY)) return NTT_ERR_ARG;
-    uint32_t *pa = static_cast<uint32_t*>(a), *pb = static_cast<uint32_t*>(b), *pc = static_cast<uint32_t*>(c);
+    uint32_t *pa = static_cast<uint32_t*>(a), *pb = static_cast<uint32_t*>(b);
     if (int rc = run_io(pa, nullptr, pa, 1, false, st)) return rc;
-    if (int rc = run_io(pb, nullptr, pb, 1, false, st)) return rc;
+    if (pb != pa)  // squaring (a == b): one forward transform, then the product of it with itself
+      if (int rc = run_io(pb, nullptr, pb, 1, false, st)) return rc;
+    return inverse_pointwise(pa, pb, c, 1, st);
+  }
+
+  // c = INTT(a * b) over `batch` transforms (the polymul's second half; a, b forward transforms).
+  // Fused: the inverse's first pass reads both transforms and multiplies at load (one HBM pass and
+  // one kernel fewer than pointwise + inverse).  c may alias a or b.
+  int inverse_pointwise(const void* a, const void* b, void* c, unsigned batch, hipStream_t st) override {
+    if (!a || !b || !c || batch == 0 || (flags & NTT_PLAN_TWIDDLE_ONLY)) return NTT_ERR_ARG;
+    auto pa = static_cast<const uint32_t*>(a), pb = static_cast<const uint32_t*>(b);
+    auto pc = static_cast<uint32_t*>(c);
     if (polymul_fusable()) {
       if (int rc = ensure_polymul_table()) return rc;
-      return run_io(pa, pb, pc, 1, true, st);
+      return run_io(pa, pb, pc, batch, true, st);
     }
-    if (int rc = pointwise(a, b, c, st)) return rc;
-    return run_io(pc, nullptr, pc, 1, true, st);
+    if (int rc = pointwise_n(pa, pb, pc, (size_t)n * batch, st)) return rc;
+    return run_io(pc, nullptr, pc, batch, true, st);
+  }
+
+  int pointwise_n(const uint32_t* a, const uint32_t* b, uint32_t* c, size_t count, hipStream_t st) {
+    const size_t off = (flags & NTT_PLAN_MONTGOMERY_IO) ? off_rm : off_r2;
+    return launch_pointwise<E>(a, b, c, count, Ff, d_tab + off, st) == hipSuccess ? NTT_OK : NTT_ERR_HIP;
   }
 
   int pointwise(const void* a, const void* b, void* c, hipStream_t st) override {
     if (!a || !b || !c) return NTT_ERR_ARG;
-    const size_t off = (flags & NTT_PLAN_MONTGOMERY_IO) ? off_rm : off_r2;
-    hipError_t e = launch_pointwise<E>(static_cast<const uint32_t*>(a), static_cast<const uint32_t*>(b),
-                                       static_cast<uint32_t*>(c), n, Ff, d_tab + off, st);
-    return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+    return pointwise_n(static_cast<const uint32_t*>(a), static_cast<const uint32_t*>(b), static_cast<uint32_t*>(c), n,
+                       st);
   }
 
   int fill(void* d, uint64_t count, int kind, uint64_t seed, uint64_t row0, unsigned log_inner, unsigned log_stride,
@@ -796,19 +812,23 @@ struct PlanImpl final : PlanBase {
   }
 
   int twiddle_pack(const void* src, void* dst, unsigned log_rows, unsigned log_len, unsigned log_bw, uint64_t row0,
-                   bool inverse, hipStream_t st) override {
+                   bool inverse, uint64_t peer_stride, hipStream_t st) override {
     if (!src || !dst || src == dst || log_bw > log_len || log_rows + log_len > 40) return NTT_ERR_ARG;
+    if (peer_stride < (1ull << (log_rows + log_bw))) return NTT_ERR_ARG;  // peer chunks must not overlap
     const uint32_t* lo = d_tab + (inverse ? off_los_i : off_los_f);
     const uint32_t* hi = d_tab + (inverse ? off_hi_i : off_hi_f);
     hipError_t e = launch_twiddle_pack<E>(static_cast<const uint32_t*>(src), static_cast<uint32_t*>(dst), log_rows,
-                                          log_len, log_bw, row0, log_n, lo, hi, lo_bits, inverse ? Fi : Ff, st);
+                                          log_len, log_bw, row0, log_n, lo, hi, lo_bits, inverse ? Fi : Ff,
+                                          peer_stride, st);
     return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
   }
 
-  int transpose(const void* src, void* dst, unsigned log_rows, unsigned log_cols, hipStream_t st) override {
-    if (!src || !dst || src == dst || log_rows + log_cols > 40) return NTT_ERR_ARG;
+  int transpose(const void* src, void* dst, unsigned log_rows, unsigned log_cols, unsigned log_blk_rows,
+                uint64_t blk_stride, hipStream_t st) override {
+    if (!src || !dst || src == dst || log_rows + log_cols > 40 || log_blk_rows > log_rows) return NTT_ERR_ARG;
+    if (blk_stride < (1ull << (log_blk_rows + log_cols))) return NTT_ERR_ARG;
     hipError_t e = launch_transpose<E>(static_cast<const uint32_t*>(src), static_cast<uint32_t*>(dst), log_rows,
-                                       log_cols, st);
+                                       log_cols, log_blk_rows, blk_stride, st);
     return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
   }
 };
@@ -827,6 +847,7 @@ static const FieldDef kFields[3] = {
 static int make_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, const uint64_t* g64, unsigned limbs64,
                      unsigned log_n, int device, unsigned flags) {
   if (log_n > 40) return NTT_ERR_ARG;
+  if (limbs64 != 1 && limbs64 != 4 && limbs64 != 6) return NTT_ERR_ARG;  // before packing into p32[12] / g32[12]
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return NTT_ERR_NODEV;
   if (device < 0 || device >= ndev) return NTT_ERR_ARG;
@@ -901,89 +922,101 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
 
 int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags) {
   if (field_id < 0 || field_id > 2) return set_err(NTT_ERR_ARG);
+  if (limbs64 != 1 && limbs64 != 4 && limbs64 != 6) return set_err(NTT_ERR_ARG);
   if (limbs64 == 1 && field_id != NTT_FIELD_P469762049) return set_err(NTT_ERR_ARG);
   const FieldDef& F = kFields[field_id];
   uint64_t p[6] = {0}, g[6] = {0};
-  const unsigned L = limbs64 > 6 ? 6 : limbs64;
-  for (unsigned i = 0; i < L && i < 4; ++i) p[i] = F.p[i];
+  for (unsigned i = 0; i < limbs64 && i < 4; ++i) p[i] = F.p[i];
   g[0] = F.g;
   return ntt_plan_create_custom_ex(out, p, g, limbs64, log_n, device, flags);
 }
 
-static int run_plan(ntt_plan* plan, void* d, unsigned batch, bool inv, void* stream) {
+// Every entry point that launches work runs it on the plan's device (saved and restored around
+// the call), so a caller whose current device differs still gets the right one.
+extern "C++" template <class F>
+static int on_device(ntt_plan* plan, F&& f) {
   if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
   int cur = 0;
   hipGetDevice(&cur);
   if (cur != plan->impl->device) hipSetDevice(plan->impl->device);
-  int rc = plan->impl->run(d, batch, inv, static_cast<hipStream_t>(stream));
+  const int rc = f(*plan->impl);
   if (cur != plan->impl->device) hipSetDevice(cur);
   return set_err(rc);
 }
 
-int ntt_forward(ntt_plan* plan, void* d_data, void* s) { return run_plan(plan, d_data, 1, false, s); }
-int ntt_inverse(ntt_plan* plan, void* d_data, void* s) { return run_plan(plan, d_data, 1, true, s); }
-int ntt_forward_batch(ntt_plan* plan, void* d_data, unsigned b, void* s) { return run_plan(plan, d_data, b, false, s); }
-int ntt_inverse_batch(ntt_plan* plan, void* d_data, unsigned b, void* s) { return run_plan(plan, d_data, b, true, s); }
+extern "C++" inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
 
-static int run_coset(ntt_plan* plan, void* d, const uint64_t* shift, bool inv, void* stream) {
-  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
-  int cur = 0;
-  hipGetDevice(&cur);
-  if (cur != plan->impl->device) hipSetDevice(plan->impl->device);
-  const unsigned limbs64 = plan->impl->elem_bytes >= 32 ? plan->impl->elem_bytes / 8 : 1;
-  int rc = plan->impl->coset(d, shift, limbs64, inv, static_cast<hipStream_t>(stream));
-  if (cur != plan->impl->device) hipSetDevice(cur);
-  return set_err(rc);
+int ntt_forward(ntt_plan* plan, void* d, void* s) {
+  return on_device(plan, [&](PlanBase& P) { return P.run(d, 1, false, S(s)); });
+}
+int ntt_inverse(ntt_plan* plan, void* d, void* s) {
+  return on_device(plan, [&](PlanBase& P) { return P.run(d, 1, true, S(s)); });
+}
+int ntt_forward_batch(ntt_plan* plan, void* d, unsigned b, void* s) {
+  return on_device(plan, [&](PlanBase& P) { return P.run(d, b, false, S(s)); });
+}
+int ntt_inverse_batch(ntt_plan* plan, void* d, unsigned b, void* s) {
+  return on_device(plan, [&](PlanBase& P) { return P.run(d, b, true, S(s)); });
+}
+
+static int run_coset(ntt_plan* plan, void* d, const uint64_t* shift, bool inv, void* s) {
+  return on_device(plan, [&](PlanBase& P) {
+    const unsigned limbs64 = P.elem_bytes >= 32 ? P.elem_bytes / 8 : 1;
+    return P.coset(d, shift, limbs64, inv, S(s));
+  });
 }
 int ntt_forward_coset(ntt_plan* plan, void* d, const uint64_t* shift, void* s) { return run_coset(plan, d, shift, false, s); }
 int ntt_inverse_coset(ntt_plan* plan, void* d, const uint64_t* shift, void* s) { return run_coset(plan, d, shift, true, s); }
 
 int ntt_pointwise_mul(ntt_plan* plan, const void* a, const void* b, void* c, void* s) {
-  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
-  return set_err(plan->impl->pointwise(a, b, c, static_cast<hipStream_t>(s)));
+  return on_device(plan, [&](PlanBase& P) { return P.pointwise(a, b, c, S(s)); });
 }
 
 int ntt_count_noncanonical(ntt_plan* plan, const void* d, uint64_t count, uint64_t* bad, void* s) {
-  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
-  int cur = 0;
-  hipGetDevice(&cur);
-  if (cur != plan->impl->device) hipSetDevice(plan->impl->device);
-  const int rc = plan->impl->count_noncanonical(d, count, bad, static_cast<hipStream_t>(s));
-  if (cur != plan->impl->device) hipSetDevice(cur);
-  return set_err(rc);
+  return on_device(plan, [&](PlanBase& P) { return P.count_noncanonical(d, count, bad, S(s)); });
 }
 
 int ntt_polymul(ntt_plan* plan, void* a, void* b, void* c, void* s) {
-  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
-  int cur = 0;
-  hipGetDevice(&cur);
-  if (cur != plan->impl->device) hipSetDevice(plan->impl->device);
-  const int rc = plan->impl->polymul(a, b, c, static_cast<hipStream_t>(s));
-  if (cur != plan->impl->device) hipSetDevice(cur);
-  return set_err(rc);
+  return on_device(plan, [&](PlanBase& P) { return P.polymul(a, b, c, S(s)); });
+}
+
+int ntt_inverse_pointwise_batch(ntt_plan* plan, const void* a, const void* b, void* c, unsigned batch, void* s) {
+  return on_device(plan, [&](PlanBase& P) { return P.inverse_pointwise(a, b, c, batch, S(s)); });
 }
 
 int ntt_fill(ntt_plan* plan, void* d, int kind, uint64_t seed, void* s) {
-  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
-  return set_err(plan->impl->fill(d, plan->impl->n, kind, seed, 0, 64, 0, static_cast<hipStream_t>(s)));
+  return on_device(plan, [&](PlanBase& P) { return P.fill(d, P.n, kind, seed, 0, 64, 0, S(s)); });
 }
 
 int ntt_fill_map(ntt_plan* plan, void* d, uint64_t count, int kind, uint64_t seed, uint64_t row0, unsigned log_inner,
                  unsigned log_stride, void* s) {
-  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
-  return set_err(plan->impl->fill(d, count, kind, seed, row0, log_inner, log_stride, static_cast<hipStream_t>(s)));
+  return on_device(plan, [&](PlanBase& P) { return P.fill(d, count, kind, seed, row0, log_inner, log_stride, S(s)); });
 }
 
 int ntt_twiddle_pack(ntt_plan* plan, const void* src, void* dst, unsigned log_rows, unsigned log_row_len,
                      unsigned log_block, uint64_t row0, int inverse, void* s) {
-  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
-  return set_err(plan->impl->twiddle_pack(src, dst, log_rows, log_row_len, log_block, row0, inverse != 0,
-                                          static_cast<hipStream_t>(s)));
+  return ntt_twiddle_pack_ex(plan, src, dst, log_rows, log_row_len, log_block, row0, inverse,
+                             1ull << (log_rows + log_block), s);
+}
+
+int ntt_twiddle_pack_ex(ntt_plan* plan, const void* src, void* dst, unsigned log_rows, unsigned log_row_len,
+                        unsigned log_block, uint64_t row0, int inverse, uint64_t peer_stride, void* s) {
+  if (log_rows + log_block >= 64) return set_err(NTT_ERR_ARG);
+  return on_device(plan, [&](PlanBase& P) {
+    return P.twiddle_pack(src, dst, log_rows, log_row_len, log_block, row0, inverse != 0, peer_stride, S(s));
+  });
 }
 
 int ntt_transpose(ntt_plan* plan, const void* src, void* dst, unsigned log_rows, unsigned log_cols, void* s) {
-  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
-  return set_err(plan->impl->transpose(src, dst, log_rows, log_cols, static_cast<hipStream_t>(s)));
+  return ntt_transpose_ex(plan, src, dst, log_rows, log_cols, log_rows, 1ull << (log_rows + log_cols), s);
+}
+
+int ntt_transpose_ex(ntt_plan* plan, const void* src, void* dst, unsigned log_rows, unsigned log_cols,
+                     unsigned log_block_rows, uint64_t block_stride, void* s) {
+  if (log_rows + log_cols >= 64) return set_err(NTT_ERR_ARG);
+  return on_device(plan, [&](PlanBase& P) {
+    return P.transpose(src, dst, log_rows, log_cols, log_block_rows, block_stride, S(s));
+  });
 }
 
 int ntt_plan_info(const ntt_plan* plan, uint64_t* n, unsigned* elem_bytes, unsigned* npasses, unsigned radix_log[8]) {

@@ -15,6 +15,11 @@ into per-peer chunks (libntt ntt_twiddle_pack) -> ONE all-to-all (RCCL; each pee
 in, row layout out), so forward/inverse/pointwise products (polynomial multiply) never leave the
 distributed layouts.  Gathering to natural order is a separate, test-only helper.
 
+Polynomial multiply (BASELINE config 5): forward(a) and forward(b) pack into one send
+buffer [G][2][r*c] so that ONE all-to-all carries both; the pointwise product is local and fused
+into the first column pass of the inverse (ntt_inverse_pointwise_batch); the inverse's all-to-all
+returns c = a*b to the row layout.  Three transforms, two exchanges.
+
 The reference has no multi-GPU code at all (no NCCL/MPI); this is new.
 The orchestration (FourStep) is engine- and transport-agnostic so the same code runs with the
 HIP engine over RCCL on GPUs, with G "virtual ranks" in one process on one GPU (exchange =
@@ -63,9 +68,11 @@ class FourStep:
     """Per-rank four-step schedule over an engine (local compute) and an exchange (all-to-all).
 
     Engine interface: ``rows_forward/rows_inverse(t, batch)`` (batched n2-point NTTs),
-    ``cols_forward/cols_inverse(t, batch)`` (batched n1-point NTTs), ``twiddle_pack(src, dst,
-    log_rows, log_len, log_block, row0, inverse)``, ``transpose(src, dst, log_rows, log_cols)``,
-    ``empty(count)``.  Exchange: ``exchange(send, recv)`` = all-to-all of equal contiguous chunks.
+    ``cols_forward/cols_inverse(t, batch)`` (batched n1-point NTTs), ``cols_inverse_pointwise(a, b,
+    out, batch)`` (out = batched n1-point INTT of a*b), ``twiddle_pack(src, dst, log_rows, log_len,
+    log_block, row0, inverse, peer_stride)``, ``transpose(src, dst, log_rows, log_cols,
+    log_block_rows, block_stride)``, ``empty(count)``.  Exchange: ``exchange(send, recv)`` =
+    all-to-all of equal contiguous chunks.
     """
 
     def __init__(self, layout: Layout, engine, exchange: Optional[Callable] = None):
@@ -74,16 +81,25 @@ class FourStep:
         self.exchange = exchange
         self.send = engine.empty(layout.local_n)
         self.recv = engine.empty(layout.local_n)
+        self.send2 = self.recv2 = None  # [G][2][chunk]: the polymul's batched exchange, on first use
+
+    @property
+    def chunk(self) -> int:
+        return self.L.r * self.L.c
 
     # ---- forward: row layout -> column layout (in place on x)
-    def forward_phase1(self, x):
+    def forward_phase1(self, x, send=None, slot: int = 0, nslots: int = 1):
         L = self.L
+        send = self.send if send is None else send
         self.eng.rows_forward(x, L.r)
-        self.eng.twiddle_pack(x, self.send, L.log_r, L.log_n2, L.log_c, L.rank * L.r, False)
+        self.eng.twiddle_pack(x, send[slot * self.chunk:], L.log_r, L.log_n2, L.log_c, L.rank * L.r, False,
+                              nslots * self.chunk)
 
-    def forward_phase2(self, x):
+    def forward_phase2(self, x, recv=None, slot: int = 0, nslots: int = 1):
         L = self.L
-        self.eng.transpose(self.recv, x, L.log_n1, L.log_c)  # recv = [G][r][c] = [n1][c]
+        recv = self.recv if recv is None else recv
+        # recv = [G][nslots][r][c]: row block g (rows g r ..) of this vector at (g nslots + slot) chunk
+        self.eng.transpose(recv[slot * self.chunk:], x, L.log_n1, L.log_c, L.log_r, nslots * self.chunk)
         self.eng.cols_forward(x, L.c)
 
     def forward(self, x):
@@ -93,14 +109,19 @@ class FourStep:
         return x
 
     # ---- inverse: column layout -> row layout (in place on x)
-    def inverse_phase1(self, x):
+    def inverse_phase1(self, x, b=None, out=None):
+        """With b: out = INTT(x * b) (the polymul's fused pointwise product); else in place on x."""
         L = self.L
-        self.eng.cols_inverse(x, L.c)
-        self.eng.twiddle_pack(x, self.send, L.log_c, L.log_n1, L.log_r, L.rank * L.c, True)
+        if b is None:
+            self.eng.cols_inverse(x, L.c)
+            out = x
+        else:
+            self.eng.cols_inverse_pointwise(x, b, out, L.c)
+        self.eng.twiddle_pack(out, self.send, L.log_c, L.log_n1, L.log_r, L.rank * L.c, True, self.chunk)
 
     def inverse_phase2(self, x):
         L = self.L
-        self.eng.transpose(self.recv, x, L.log_n2, L.log_r)  # recv = [G][c][r] = [n2][r]
+        self.eng.transpose(self.recv, x, L.log_n2, L.log_r, L.log_n2, L.local_n)  # recv = [G][c][r] = [n2][r]
         self.eng.rows_inverse(x, L.r)
 
     def inverse(self, x):
@@ -109,6 +130,39 @@ class FourStep:
         self.inverse_phase2(x)
         return x
 
+    # ---- polynomial multiply: row-layout a, b -> row-layout out = a * b (cyclic, length n).
+    # a and b are left holding their column-layout forward transforms (unless out aliases them).
+    def pair_buffers(self):
+        if self.send2 is None:
+            self.send2 = self.eng.empty(2 * self.L.local_n)
+            self.recv2 = self.eng.empty(2 * self.L.local_n)
+        return self.send2, self.recv2
+
+    def polymul_phase1(self, a, b):
+        if a is b:
+            self.forward_phase1(a)
+            return self.send, self.recv
+        send2, recv2 = self.pair_buffers()
+        self.forward_phase1(a, send2, 0, 2)
+        self.forward_phase1(b, send2, 1, 2)
+        return send2, recv2
+
+    def polymul_phase2(self, a, b, out):
+        if a is b:
+            self.forward_phase2(a)
+        else:
+            self.forward_phase2(a, self.recv2, 0, 2)
+            self.forward_phase2(b, self.recv2, 1, 2)
+        self.inverse_phase1(a, b, out)
+
+    def polymul(self, a, b, out):
+        send, recv = self.polymul_phase1(a, b)
+        self.exchange(send, recv)
+        self.polymul_phase2(a, b, out)
+        self.exchange(self.send, self.recv)
+        self.inverse_phase2(out)
+        return out
+
 
 class HipEngine:
     """Local steps on one GPU through libntt (the product path)."""
@@ -116,8 +170,10 @@ class HipEngine:
     def __init__(self, field_id: int, log_n: int, limbs64: int, world: int, device: int):
         from .ntt import NTTPlan
         L = Layout(log_n, world, 0)
+        # separate row and column plans even when n1 == n2: their per-launch timing rings then hold
+        # one kernel shape each (bench.py reports them apart)
         self.rows = NTTPlan(field_id, L.log_n2, limbs64, device)
-        self.cols = self.rows if L.log_n1 == L.log_n2 else NTTPlan(field_id, L.log_n1, limbs64, device)
+        self.cols = NTTPlan(field_id, L.log_n1, limbs64, device)
         self.tw = NTTPlan(field_id, log_n, limbs64, device, twiddle_only=True)
         self.limbs64 = limbs64
         self.device = device
@@ -138,14 +194,17 @@ class HipEngine:
     def cols_inverse(self, t, batch):
         self.cols.inverse_batch(t, batch)
 
-    def twiddle_pack(self, src, dst, log_rows, log_len, log_block, row0, inverse):
-        self.tw.twiddle_pack(src, dst, log_rows, log_len, log_block, row0, inverse)
+    def cols_inverse_pointwise(self, a, b, out, batch):
+        self.cols.inverse_pointwise_batch(a, b, out, batch)
 
-    def transpose(self, src, dst, log_rows, log_cols):
-        self.tw.transpose(src, dst, log_rows, log_cols)
+    def twiddle_pack(self, src, dst, log_rows, log_len, log_block, row0, inverse, peer_stride=None):
+        self.tw.twiddle_pack(src, dst, log_rows, log_len, log_block, row0, inverse, peer_stride=peer_stride)
+
+    def transpose(self, src, dst, log_rows, log_cols, log_block_rows=None, block_stride=None):
+        self.tw.transpose(src, dst, log_rows, log_cols, log_block_rows=log_block_rows, block_stride=block_stride)
 
     def plans(self):
-        return [self.rows] if self.cols is self.rows else [self.rows, self.cols]
+        return [self.rows, self.cols]
 
 
 class DistNTT:
@@ -173,8 +232,23 @@ class DistNTT:
         self.n = self.layout.n
         self.passes = self.engine.rows.passes
 
+    # RCCL moves < 2 GiB per peer per collective (a 2 GiB chunk arrived half copied,
+    # tests/test_gpu_fullsize.py): larger per-peer chunks go as several all-to-alls of pieces.
+    MAX_PEER_BYTES = 1 << 30
+
     def _exchange(self, send, recv):
-        self.dist.all_to_all_single(recv.view(-1), send.view(-1), group=self.group)
+        s, r = send.view(-1), recv.view(-1)
+        world = self.layout.world
+        per = s.numel() // world  # int64 words per peer
+        if per * 8 <= self.MAX_PEER_BYTES:
+            self.dist.all_to_all_single(r, s, group=self.group)
+            return
+        sv, rv = s.view(world, per), r.view(world, per)
+        piece = self.MAX_PEER_BYTES // 8
+        for off in range(0, per, piece):
+            cnt = min(piece, per - off)
+            self.dist.all_to_all([rv[g, off:off + cnt] for g in range(world)],
+                                 [sv[g, off:off + cnt] for g in range(world)], group=self.group)
 
     def empty(self) -> torch.Tensor:
         return self.engine.empty(self.layout.local_n)
@@ -190,6 +264,10 @@ class DistNTT:
 
     def inverse(self, t: torch.Tensor) -> torch.Tensor:
         return self.fs.inverse(t)
+
+    def polymul(self, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """Row-layout shares a, b -> row-layout share of c = a * b (cyclic, length n); two all-to-alls."""
+        return self.fs.polymul(a, b, out)
 
     def set_profiling(self, enable: bool = True) -> None:
         for p in self.engine.plans():
@@ -214,13 +292,14 @@ class VirtualRanks:
         self.ranks = [FourStep(Layout(log_n, world, g), self.engine) for g in range(world)]
         self.layout0 = self.ranks[0].L
 
-    def _exchange_all(self):
+    def _exchange_all(self, sends=None, recvs=None):
         G = self.world
-        chunk = self.layout0.local_n // G
+        sends = sends or [fs.send for fs in self.ranks]
+        recvs = recvs or [fs.recv for fs in self.ranks]
+        chunk = sends[0].shape[0] // G
         for dst in range(G):
             for src in range(G):
-                self.ranks[dst].recv[src * chunk:(src + 1) * chunk].copy_(
-                    self.ranks[src].send[dst * chunk:(dst + 1) * chunk])
+                recvs[dst][src * chunk:(src + 1) * chunk].copy_(sends[src][dst * chunk:(dst + 1) * chunk])
 
     def empty(self) -> List[torch.Tensor]:
         return [self.engine.empty(self.layout0.local_n) for _ in range(self.world)]
@@ -246,6 +325,16 @@ class VirtualRanks:
         for fs, x in zip(self.ranks, xs):
             fs.inverse_phase2(x)
         return xs
+
+    def polymul(self, As: List[torch.Tensor], Bs: List[torch.Tensor], Outs: List[torch.Tensor]):
+        bufs = [fs.polymul_phase1(a, b) for fs, a, b in zip(self.ranks, As, Bs)]
+        self._exchange_all([s for s, _ in bufs], [r for _, r in bufs])
+        for fs, a, b, o in zip(self.ranks, As, Bs, Outs):
+            fs.polymul_phase2(a, b, o)
+        self._exchange_all()
+        for fs, o in zip(self.ranks, Outs):
+            fs.inverse_phase2(o)
+        return Outs
 
 
 class MultiPlan:
@@ -305,3 +394,11 @@ class MultiPlan:
         data, streams = self._ptrs(xs)
         self._L.check(self.lib.ntt_inverse_multi(self.handle, data, streams), "ntt_inverse_multi")
         return xs
+
+    def polymul(self, As, Bs, Outs):
+        """Row-layout shares of a, b -> row-layout shares of c = a * b (ntt_polymul_multi)."""
+        a, streams = self._ptrs(As)
+        b, _ = self._ptrs(Bs)
+        c, _ = self._ptrs(Outs)
+        self._L.check(self.lib.ntt_polymul_multi(self.handle, a, b, c, streams), "ntt_polymul_multi")
+        return Outs

@@ -59,6 +59,11 @@ PROTOTYPES = {
     "ntt_mplan_info": (C.c_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint), C.POINTER(C.c_uint)]),
     "ntt_mplan_destroy": (C.c_int, [_vp]),
     "ntt_count_noncanonical": (C.c_int, [_vp, _vp, C.c_uint64, C.POINTER(C.c_uint64), _vp]),
+    "ntt_inverse_pointwise_batch": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint, _vp]),
+    "ntt_twiddle_pack_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint, C.c_uint, C.c_uint, C.c_uint64, C.c_int, C.c_uint64,
+                                      _vp]),
+    "ntt_transpose_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint, C.c_uint, C.c_uint, C.c_uint64, _vp]),
+    "ntt_polymul_multi": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp)]),
 }
 
 _lock = threading.Lock()

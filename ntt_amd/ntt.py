@@ -190,6 +190,16 @@ class NTTPlan:
                                        C.c_void_p(out.data_ptr()), _stream_ptr(stream, a.device)), "ntt_polymul")
         return out
 
+    def inverse_pointwise_batch(self, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, batch: int,
+                                stream=None) -> torch.Tensor:
+        """out = INTT(a * b) over `batch` transforms (a, b already forward-transformed)."""
+        for t in (a, b, out):
+            self._check_tensor(t, batch)
+        _L.check(self._lib.ntt_inverse_pointwise_batch(self._h, C.c_void_p(a.data_ptr()), C.c_void_p(b.data_ptr()),
+                                                       C.c_void_p(out.data_ptr()), int(batch),
+                                                       _stream_ptr(stream, a.device)), "ntt_inverse_pointwise_batch")
+        return out
+
     def fill(self, t: torch.Tensor, kind: str = "random", seed: int = 1, stream=None) -> torch.Tensor:
         """SURVEY §8d synthetic inputs on the device: 'iota' (x_j = j) or 'random' (SplitMix64)."""
         self._check_tensor(t)
@@ -209,17 +219,25 @@ class NTTPlan:
         return t
 
     def twiddle_pack(self, src: torch.Tensor, dst: torch.Tensor, log_rows: int, log_row_len: int, log_block: int,
-                     row0: int, inverse: bool = False, stream=None) -> torch.Tensor:
-        """dst[b >> log_block][a][b & m] = src[a][b] * w_n^(+-(row0 + a) * b) (four-step twiddle + pack)."""
-        _L.check(self._lib.ntt_twiddle_pack(self._h, C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()),
-                                            int(log_rows), int(log_row_len), int(log_block), int(row0),
-                                            int(bool(inverse)), _stream_ptr(stream, src.device)), "ntt_twiddle_pack")
+                     row0: int, inverse: bool = False, stream=None, peer_stride: Optional[int] = None) -> torch.Tensor:
+        """dst[q * peer_stride + a * bw + b % bw] = src[a][b] * w_n^(+-(row0 + a) * b), q = b >> log_block
+        (four-step twiddle + pack; peer_stride defaults to the dense 2^(log_rows + log_block))."""
+        ps = (1 << (log_rows + log_block)) if peer_stride is None else int(peer_stride)
+        _L.check(self._lib.ntt_twiddle_pack_ex(self._h, C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()),
+                                               int(log_rows), int(log_row_len), int(log_block), int(row0),
+                                               int(bool(inverse)), ps, _stream_ptr(stream, src.device)),
+                 "ntt_twiddle_pack_ex")
         return dst
 
-    def transpose(self, src: torch.Tensor, dst: torch.Tensor, log_rows: int, log_cols: int, stream=None):
-        _L.check(self._lib.ntt_transpose(self._h, C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()),
-                                         int(log_rows), int(log_cols), _stream_ptr(stream, src.device)),
-                 "ntt_transpose")
+    def transpose(self, src: torch.Tensor, dst: torch.Tensor, log_rows: int, log_cols: int, stream=None,
+                  log_block_rows: Optional[int] = None, block_stride: Optional[int] = None):
+        """dst[c][r] = src row r, column c; source rows in blocks of 2^log_block_rows starting every
+        block_stride elements (default: one dense [rows][cols] matrix)."""
+        lb = log_rows if log_block_rows is None else int(log_block_rows)
+        bs = (1 << (lb + log_cols)) if block_stride is None else int(block_stride)
+        _L.check(self._lib.ntt_transpose_ex(self._h, C.c_void_p(src.data_ptr()), C.c_void_p(dst.data_ptr()),
+                                            int(log_rows), int(log_cols), lb, bs, _stream_ptr(stream, src.device)),
+                 "ntt_transpose_ex")
         return dst
 
     def set_profiling(self, enable: bool = True) -> None:

@@ -38,21 +38,33 @@ class CpuOracleEngine:
     cols_forward = rows_forward
     cols_inverse = rows_inverse
 
-    def twiddle_pack(self, src, dst, log_rows, log_len, log_block, row0, inverse):
+    def cols_inverse_pointwise(self, a, b, out, batch):
+        n = a.shape[0] // batch
+        prod = OC.mul_mp(a.numpy().view(np.uint64).reshape(-1, self.L), b.numpy().view(np.uint64).reshape(-1, self.L),
+                         self.p)
+        for i in range(batch):
+            prod[i * n:(i + 1) * n] = OC.ntt_mp(prod[i * n:(i + 1) * n], self.p, self.g, True)
+        out.numpy().view(np.uint64).reshape(-1, self.L)[:] = prod
+
+    def twiddle_pack(self, src, dst, log_rows, log_len, log_block, row0, inverse, peer_stride=None):
         n = 1 << self.log_n
         table = self.pw_inv if inverse else self.pw
         s = OC.limbs_to_ints(src.numpy().view(np.uint64).reshape(-1, self.L))
-        out = [0] * len(s)
         rows, length, bw = 1 << log_rows, 1 << log_len, 1 << log_block
+        ps = rows * bw if peer_stride is None else peer_stride
+        d = dst.numpy().view(np.uint64).reshape(-1, self.L)
         for a in range(rows):
             for b in range(length):
                 v = s[a * length + b] * table[((row0 + a) * b) % n] % self.p
-                out[(b // bw) * rows * bw + a * bw + (b % bw)] = v
-        dst.numpy().view(np.uint64)[:] = OC.ints_to_limbs(out, self.L).reshape(dst.shape)
+                d[(b // bw) * ps + a * bw + (b % bw)] = OC.ints_to_limbs([v], self.L)[0]
 
-    def transpose(self, src, dst, log_rows, log_cols):
-        a = src.numpy().view(np.uint64).reshape(1 << log_rows, 1 << log_cols, self.L)
-        dst.numpy().view(np.uint64)[:] = np.ascontiguousarray(a.transpose(1, 0, 2)).reshape(dst.shape)
+    def transpose(self, src, dst, log_rows, log_cols, log_block_rows=None, block_stride=None):
+        lb = log_rows if log_block_rows is None else log_block_rows
+        bs = (1 << (lb + log_cols)) if block_stride is None else block_stride
+        s = src.numpy().view(np.uint64).reshape(-1, self.L)
+        rows, cols = 1 << log_rows, 1 << log_cols
+        m = np.stack([s[(r >> lb) * bs + (r & ((1 << lb) - 1)) * cols:][:cols] for r in range(rows)])
+        dst.numpy().view(np.uint64).reshape(-1, self.L)[:] = np.ascontiguousarray(m.transpose(1, 0, 2)).reshape(-1, self.L)
 
 
 def row_shares(x_ints, layout_cls, log_n, world, L):

@@ -79,3 +79,26 @@ def test_mplan_create_fails_cleanly_without_gpu_or_bad_args():
     assert st in (-5, -2, -1) and not h.value
     assert so.ntt_forward_multi(None, None, None) == -1
     assert so.ntt_mplan_destroy(None) == 0
+
+
+def test_limb_counts_outside_1_4_6_are_rejected_before_any_packing():
+    """limbs64 >= 7 used to overrun the 12-word modulus buffers; now NTT_ERR_ARG."""
+    from ntt_amd import lib as L
+    so = L.load()
+    h = C.c_void_p()
+    for limbs in (0, 2, 3, 5, 7, 8, 64):
+        assert so.ntt_plan_create_ex(C.byref(h), 1, 10, limbs, 0, 0) == -1, limbs
+        p = (C.c_uint64 * 8)(*([0xFFFFFFFF00000001] + [0] * 7))
+        g = (C.c_uint64 * 8)(*([7] + [0] * 7))
+        assert so.ntt_plan_create_custom(C.byref(h), p, g, limbs, 10, 0) == -1, limbs
+        assert not h.value
+
+
+def test_compiled_c_caller_builds_against_header_and_library():
+    """tests/c/dropin.c (a plain-C caller of include/ntt.h) compiles with -Werror and links
+    libntt.so: the header is valid C and every symbol it calls is exported."""
+    import shutil
+    if not shutil.which("gcc") or not os.path.exists("/opt/rocm/include/hip/hip_runtime_api.h"):
+        pytest.skip("gcc / ROCm headers unavailable")
+    from tests.dropin_build import build
+    assert os.access(build(), os.X_OK)

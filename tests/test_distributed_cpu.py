@@ -90,3 +90,62 @@ def test_layout_rejects_bad_world():
         Layout(10, 3, 0)
     with pytest.raises(ValueError):
         Layout(4, 8, 0)
+
+
+def _polymul_worker(rank, world, port, field_id, log_n, L, square, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from ntt_amd.distributed import FourStep, Layout
+    from tests.dist_helpers import CpuOracleEngine, row_shares
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 1 << log_n
+        a = R.random_vector(field_id, n, seed=5)
+        b = a if square else R.random_vector(field_id, n, seed=6)
+        sa = row_shares(a, Layout, log_n, world, L)[rank]
+        sb = sa if square else row_shares(b, Layout, log_n, world, L)[rank]
+        out = torch.zeros_like(sa)
+        eng = CpuOracleEngine(field_id, log_n, L)
+        fs = FourStep(Layout(log_n, world, rank), eng, lambda s, r: dist.all_to_all_single(r.view(-1), s.view(-1)))
+        fs.polymul(sa, sb, out)
+        q.put((rank, out.numpy().tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,field_id,log_n,square", [(2, 1, 6, False), (4, 1, 8, False), (2, 2, 7, True)])
+def test_distributed_polymul_gloo(world, field_id, log_n, square):
+    """C5's schedule (forward(a), forward(b) in ONE all-to-all, local pointwise product fused into
+    the inverse, inverse all-to-all) over gloo: the row-layout result equals the oracle's cyclic
+    product; squaring (a is b) takes the single-vector exchange."""
+    import numpy as np
+    from ntt_amd.distributed import Layout
+    L = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_polymul_worker, args=(r, world, port, field_id, log_n, L, square, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rank, out = q.get(timeout=240)
+        res[rank] = out
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = 1 << log_n
+    p_, g_ = R.FIELDS[field_id]
+    a = R.random_vector(field_id, n, seed=5)
+    b = a if square else R.random_vector(field_id, n, seed=6)
+    exp = R.polymul(a, b, p_, g_)
+    got = [None] * n
+    for r in range(world):
+        lay = Layout(log_n, world, r)
+        vals = OC.limbs_to_ints(np.frombuffer(res[r], dtype=np.uint64).reshape(-1, L))
+        for i, v in enumerate(vals):
+            got[lay.row_global(i)] = v
+    assert got == exp

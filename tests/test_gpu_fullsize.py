@@ -1,0 +1,106 @@
+"""Full-size GPU parity, element by element and for the multi-GPU configs.
+
+* 2^24 random vectors compared with the threaded C oracle (oracle_ntt_mp_par, a restatement of
+  GZKP-NTT.cu:30-48 pinned in test_oracle.py / test_oracle_ref.py): BN254 forward and inverse (the
+  headline), BLS12-381 Fr forward and inverse in the 6 x 64-bit layout (C3), the 8-B P path at 2^26;
+* C4's four-step at 2^28 over 8 virtual ranks (one GPU, exchange = device copies): the closed-form
+  KAT of x_j = j at sampled k of the gathered column layout, plus the inverse round trip;
+* the single-process multi-GPU plan (ntt_mplan_*, RCCL) at 2^26 and 2^28 on the visible devices.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ntt_ref as R
+from oracle import oracle_c as OC
+
+pytestmark = pytest.mark.gpu
+THREADS = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "8"))))
+
+
+def _plan(fid, log_n, L):
+    from ntt_amd.ntt import NTTPlan
+    return NTTPlan(field_id=fid, log_n=log_n, limbs64=L, device=0)
+
+
+def _host(t, L):
+    return t.cpu().numpy().view(np.uint64).reshape(-1, L)
+
+
+@pytest.mark.parametrize("fid,L,seed", [(1, 4, 24), (2, 6, 3)])
+def test_2pow24_elementwise_vs_threaded_oracle(fid, L, seed):
+    p, g = R.FIELDS[fid]
+    pl = _plan(fid, 24, L)
+    t = pl.empty()
+    pl.fill(t, "random", seed=seed)
+    x = _host(t, L).copy()
+    pl.forward(t)
+    exp = OC.ntt_mp_par(x, p, g, THREADS)
+    assert np.array_equal(_host(t, L), exp), (fid, L, "forward")
+    del exp
+    t.copy_(torch.from_numpy(x.view(np.int64)).to(t.device))
+    pl.inverse(t)
+    exp = OC.ntt_mp_par(x, p, g, THREADS, inverse=True)
+    assert np.array_equal(_host(t, L), exp), (fid, L, "inverse")
+
+
+def test_p_path_2pow26_elementwise():
+    p, g = R.FIELDS[0]
+    pl = _plan(0, 26, 1)
+    t = pl.empty()
+    pl.fill(t, "random", seed=26)
+    x = t.cpu().numpy().copy()
+    pl.forward(t)
+    assert np.array_equal(t.cpu().numpy(), OC.ntt_u64(x, p, g))
+    pl.inverse(t)
+    assert np.array_equal(t.cpu().numpy(), x)
+
+
+def _kat_check_columns(shares, layouts, n, p, g, L, ks):
+    for k in ks:
+        k2, k1 = k % layouts[0].n2, k // layouts[0].n2
+        rank, kc = k2 // layouts[0].c, k2 % layouts[0].c
+        row = shares[rank][kc * layouts[0].n1 + k1].cpu().numpy().view(np.uint64).reshape(-1)
+        v = sum(int(row[i]) << (64 * i) for i in range(L))
+        assert v == R.kat_xj(n, p, g, k), k
+
+
+def _row_index(lay, device):
+    i = torch.arange(lay.local_n, dtype=torch.int64, device=device)
+    return lay.rank * lay.r + (i >> lay.log_n2) + lay.n1 * (i & (lay.n2 - 1))
+
+
+def test_c4_fourstep_2pow28_eight_virtual_ranks():
+    from ntt_amd.distributed import VirtualRanks
+    fid, L, log_n, world = 1, 4, 28, 8
+    p, g = R.FIELDS[fid]
+    n = 1 << log_n
+    vr = VirtualRanks(fid, log_n, L, world)
+    xs = vr.fill(vr.empty(), "iota")
+    vr.forward(xs)
+    rng = np.random.default_rng(4)
+    ks = [0, 1, 2, 3, n // 2, n - 1] + [int(k) for k in rng.integers(0, n, 30)]
+    _kat_check_columns(xs, [fs.L for fs in vr.ranks], n, p, g, L, ks)
+    vr.inverse(xs)
+    for fs, t in zip(vr.ranks, xs):
+        assert torch.equal(t[:, 0], _row_index(fs.L, t.device)) and not bool(t[:, 1:].any()), fs.L.rank
+
+
+@pytest.mark.parametrize("log_n", [26, 28])
+def test_mplan_large_kat_and_round_trip(log_n):
+    from ntt_amd.distributed import MultiPlan
+    fid, L = 1, 4
+    p, g = R.FIELDS[fid]
+    n = 1 << log_n
+    mp = MultiPlan(fid, log_n, L, devices=list(range(torch.cuda.device_count())))
+    xs = mp.fill(mp.empty(), "iota")
+    mp.forward(xs)
+    rng = np.random.default_rng(log_n)
+    ks = [0, 1, 2, 3, n // 2, n - 1] + [int(k) for k in rng.integers(0, n, 30)]
+    _kat_check_columns(xs, mp.layouts, n, p, g, L, ks)
+    mp.inverse(xs)
+    for lay, t in zip(mp.layouts, xs):
+        assert torch.equal(t[:, 0], _row_index(lay, t.device)) and not bool(t[:, 1:].any())
+    del mp

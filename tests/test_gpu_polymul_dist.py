@@ -1,0 +1,130 @@
+"""Polynomial multiply on the GPU: squaring (a == b) on one GPU, and the distributed polymul of
+BASELINE config 5 (forward(a), forward(b) in ONE all-to-all, local pointwise product
+fused into the inverse's first column pass, inverse all-to-all back to the row layout).
+
+The distributed result is compared bit for bit with the single-GPU ntt_polymul of the same vectors
+(itself checked against the oracle's cyclic product in test_gpu_parity.py and below), through
+virtual ranks (one GPU, exchange = device copies) at G = 1..8 up to C5's 2^24, the single-process
+multi-GPU plan (ntt_polymul_multi, RCCL) and DistNTT over a torch.distributed RCCL group.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ntt_ref as R
+from oracle import oracle_c as OC
+
+pytestmark = pytest.mark.gpu
+
+
+def _plan(fid, log_n, L):
+    from ntt_amd.ntt import NTTPlan
+    return NTTPlan(field_id=fid, log_n=log_n, limbs64=L, device=0)
+
+
+def _host(t, L):
+    return t.cpu().numpy().view(np.uint64).reshape(-1, L)
+
+
+@pytest.mark.parametrize("fid,L,log_n", [(1, 4, 12), (1, 4, 16), (2, 6, 13), (0, 1, 14), (0, 4, 12)])
+def test_single_gpu_squaring_matches_oracle(fid, L, log_n):
+    """polymul(a, a, c) used to forward-transform a twice."""
+    p, g = R.FIELDS[fid]
+    pl = _plan(fid, log_n, L)
+    a = pl.fill(pl.empty(), "random", seed=80 + log_n)
+    x = _host(a, L).copy()
+    c = pl.empty()
+    pl.polymul(a, a, c)
+    if L == 1:
+        A = OC.ntt_u64(x[:, 0].astype(np.int64), p, g)
+        C2 = np.array([int(u) * int(u) % p for u in A], dtype=np.int64)
+        exp = OC.ntt_u64(C2, p, g, True).astype(np.uint64).reshape(-1, 1)
+    else:
+        A = OC.ntt_mp(x, p, g)
+        exp = OC.ntt_mp(OC.mul_mp(A, A, p), p, g, inverse=True)
+    assert np.array_equal(_host(c, L), exp)
+
+
+def _row_index(lay, device):
+    i = torch.arange(lay.local_n, dtype=torch.int64, device=device)
+    return lay.rank * lay.r + (i >> lay.log_n2) + lay.n1 * (i & (lay.n2 - 1))
+
+
+def _single_gpu_product(fid, L, log_n, seed_a, seed_b):
+    pl = _plan(fid, log_n, L)
+    a = pl.fill(pl.empty(), "random", seed=seed_a)
+    b = a if seed_b is None else pl.fill(pl.empty(), "random", seed=seed_b)
+    c = pl.empty()
+    pl.polymul(a, b, c)
+    return c
+
+
+@pytest.mark.parametrize("world,fid,L,log_n,square", [(1, 1, 4, 12, False), (2, 1, 4, 13, False),
+                                                      (4, 1, 4, 16, False), (8, 1, 4, 20, False),
+                                                      (8, 2, 6, 16, False), (2, 0, 1, 14, False),
+                                                      (4, 1, 4, 14, True)])
+def test_virtual_ranks_polymul_matches_single_gpu(world, fid, L, log_n, square):
+    from ntt_amd.distributed import VirtualRanks
+    exp = _single_gpu_product(fid, L, log_n, 5, None if square else 6)
+    vr = VirtualRanks(fid, log_n, L, world)
+    As = vr.fill(vr.empty(), "random", seed=5)
+    Bs = As if square else vr.fill(vr.empty(), "random", seed=6)
+    Outs = vr.empty()
+    vr.polymul(As, Bs, Outs)
+    for fs, o in zip(vr.ranks, Outs):
+        assert torch.equal(o, exp[_row_index(fs.L, o.device)]), (world, log_n, fs.L.rank)
+
+
+def test_c5_polymul_2pow24_eight_virtual_ranks():
+    """BASELINE config 5's size and GPU count, on one GPU: bit-exact vs the single-GPU product."""
+    from ntt_amd.distributed import VirtualRanks
+    fid, L, log_n, world = 1, 4, 24, 8
+    exp = _single_gpu_product(fid, L, log_n, 5, 6)
+    vr = VirtualRanks(fid, log_n, L, world)
+    As = vr.fill(vr.empty(), "random", seed=5)
+    Bs = vr.fill(vr.empty(), "random", seed=6)
+    vr.polymul(As, Bs, As)  # out aliases a
+    for fs, o in zip(vr.ranks, As):
+        assert torch.equal(o, exp[_row_index(fs.L, o.device)]), fs.L.rank
+
+
+@pytest.mark.parametrize("log_n", [16, 24])
+def test_mplan_polymul_matches_single_gpu(log_n):
+    from ntt_amd.distributed import MultiPlan
+    fid, L = 1, 4
+    exp = _single_gpu_product(fid, L, log_n, 5, 6)
+    mp = MultiPlan(fid, log_n, L, devices=list(range(torch.cuda.device_count())))
+    As = mp.fill(mp.empty(), "random", seed=5)
+    Bs = mp.fill(mp.empty(), "random", seed=6)
+    Outs = mp.empty()
+    mp.polymul(As, Bs, Outs)
+    for lay, o in zip(mp.layouts, Outs):
+        assert torch.equal(o.to("cuda:0"), exp[_row_index(lay, "cuda:0")]), lay.rank
+    # squaring through the same entry point (a == b: one forward, single-vector exchange)
+    exp2 = _single_gpu_product(fid, L, log_n, 5, None)
+    As = mp.fill(mp.empty(), "random", seed=5)
+    mp.polymul(As, As, Outs)
+    for lay, o in zip(mp.layouts, Outs):
+        assert torch.equal(o.to("cuda:0"), exp2[_row_index(lay, "cuda:0")]), lay.rank
+    del mp
+
+
+def test_dist_ntt_polymul_rccl_world1():
+    import torch.distributed as dist
+    from ntt_amd.distributed import DistNTT
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = "29563"
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        log_n = 18
+        exp = _single_gpu_product(1, 4, log_n, 5, 6)
+        d = DistNTT(1, log_n, 4, device=0)
+        a = d.fill(d.empty(), "random", seed=5)
+        b = d.fill(d.empty(), "random", seed=6)
+        out = d.empty()
+        d.polymul(a, b, out)
+        assert torch.equal(out, exp[_row_index(d.layout, "cuda:0")])
+    finally:
+        dist.destroy_process_group()

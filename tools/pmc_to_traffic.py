@@ -4,7 +4,9 @@ For the bench's NTT step, the kernel launches of one transform repeat in a fixed
 passes, then the final pass).  Per-dispatch HBM bytes = 2 * FETCH_SIZE * 1024 (gfx950 reports half
 of a wide coalesced stream, MI355X_MICROARCH.md §HBM) + WRITE_SIZE * 1024, taken from the separate
 fetch and write passes and matched by dispatch order.  Writes profiles/pmc_summary.json:
-    {tag: [bytes of launch 0, launch 1, ...]}
+    {tag: {"launch_bytes": [bytes of launch 0, launch 1, ...], "src_hash": H, "profile": DIR}}
+where H = ntt_amd.build.source_hash() of the tree that was profiled (bench.py reports the bytes only
+while the kernel sources still hash to H).
 Usage: python tools/pmc_to_traffic.py gpurun_out/pmc TAG [profiles/pmc_summary.json]
 """
 import csv
@@ -44,8 +46,10 @@ def main():
         f = [fetch[s * per + i][1] for s in range(1, steps)] or [fetch[i][1]]
         w = [write[s * per + i][1] for s in range(1, steps)] or [write[i][1]]
         traffic.append(2 * 1024 * sum(f) / len(f) + 1024 * sum(w) / len(w))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from ntt_amd.build import source_hash
     d = json.load(open(out)) if os.path.exists(out) else {}
-    d[tag] = traffic
+    d[tag] = {"launch_bytes": traffic, "src_hash": source_hash(), "profile": root}
     json.dump(d, open(out, "w"), indent=1)
     print(tag, [f"{t / 1e9:.3f} GB" for t in traffic])
 
