@@ -8,7 +8,8 @@ One JSON line per config:
   C4  2^28 forward, BN254 Fr: on one GPU as a plain transform, and as the partitioned four-step
       with 8 virtual ranks on one device (device copies stand in for the RCCL all-to-all; the
       all-to-all over xGMI is timed only by bench.py --four-step on a multi-GPU node)
-  C5  polynomial multiply of length 2^24 (2 forward + pointwise + inverse), BN254 Fr
+  C5  polynomial multiply of length 2^24 (2 forward + pointwise + inverse), BN254 Fr, on one GPU
+      and as the distributed schedule over 8 virtual ranks
   +   2^24 coset forward (low-degree extension), BN254 Fr
 Timing: W warmups, then K runs bracketed by torch.cuda.synchronize(); inputs resident in HBM.
 """
@@ -112,6 +113,15 @@ def main():
     emit("C5: polymul length 2^24 BN254 Fr (2 forward + pointwise + inverse), one GPU", 1 << 24,
          timeit(lambda: pl.polymul(a, b, c)))
     emit("coset forward 2^24 BN254 Fr (shift = generator 5)", 1 << 24, timeit(lambda: pl.forward_coset(a, 5)))
+    del pl, a, b, c
+    torch.cuda.empty_cache()
+    vr = VirtualRanks(1, 24, 4, 8)
+    As = vr.fill(vr.empty(), "random", seed=5)
+    Bs = vr.fill(vr.empty(), "random", seed=6)
+    Cs = vr.empty()
+    emit("C5: polymul length 2^24 BN254 Fr, distributed schedule over 8 virtual ranks on one GPU", 1 << 24,
+         timeit(lambda: vr.polymul(As, Bs, Cs), 5, 10),
+         note="2 exchanges (a and b batched in one) as device copies; RCCL timing needs a multi-GPU node")
 
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     with open(args.out, "w") as f:

@@ -29,5 +29,7 @@ if [ "$WHAT" = bench ] || [ "$WHAT" = all ]; then
   step pmc_write 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc/write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
   step traffic 60 python -u tools/pmc_to_traffic.py $O/pmc f1_L4_n24_w1 $O/pmc_summary.json
   step configs 600 python -u tools/bench_configs.py --out $O/configs.jsonl
+  # the N > 1 default (partitioned four-step over RCCL), rehearsed at world size 1
+  step bench_fourstep_w1 300 python -u bench.py --four-step --steps 20 --warmup 10 --no-cpu-baseline
 fi
 echo "[round_gpu] done" >&2
