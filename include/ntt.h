@@ -167,14 +167,46 @@ int NTT_GZKP_64(long long* data, const void* reverse, long long len, long long o
                 long long reverse_num);
 int ntt_last_error(void);
 
+/* ---------------------------------------------------------------- one rank of the distributed four-step
+ * New (the reference has no multi-GPU code).  The local steps of rank `rank` of `world`
+ * around the all-to-all, fused so that no separate twiddle, pack or transpose pass runs: the row
+ * transforms' last pass applies w_n^(j1 k2) and stores straight into the peer chunks, and the column
+ * transforms read the received chunks in place (2^log_c interleaved transforms).  Layouts as the
+ * multi-GPU plan below: row layout [r][n2], column layout [n1][c].  Send / receive buffers are the
+ * caller's: [world][nvec][chunk] elements (chunk = r c, ntt_rplan_info), exchanged by the caller
+ * as ONE all-to-all of equal chunks (RCCL, device copies, ...).  nvec = 2 carries two vectors per
+ * exchange (polymul: slot 0 = a, slot 1 = b).  All calls are asynchronous on hip_stream. */
+typedef struct ntt_rplan ntt_rplan;
+int ntt_rplan_create(ntt_rplan** out, int field_id, unsigned log_n, unsigned limbs64, int world, int rank,
+                     int device);
+int ntt_rplan_info(const ntt_rplan* rp, uint64_t* local_n, uint64_t* chunk, unsigned* log_n1, unsigned* log_n2,
+                   unsigned* elem_bytes);
+/* row layout x (unchanged) -> send slot `slot` of nvec */
+int ntt_rplan_forward_rows(ntt_rplan* rp, const void* d_x, void* d_send, unsigned nvec, unsigned slot,
+                           void* hip_stream);
+/* recv slot `slot` of nvec -> column layout x */
+int ntt_rplan_forward_cols(ntt_rplan* rp, const void* d_recv, void* d_x, unsigned nvec, unsigned slot,
+                           void* hip_stream);
+/* column layout x (times y, pointwise, when y != NULL: the polymul's product) -> send (nvec = 1) */
+int ntt_rplan_inverse_cols(ntt_rplan* rp, const void* d_x, const void* d_y, void* d_send, void* hip_stream);
+/* recv (nvec = 1) -> row layout out (1/n included over both halves) */
+int ntt_rplan_inverse_rows(ntt_rplan* rp, const void* d_recv, void* d_out, void* hip_stream);
+/* this rank's row-layout share of the global synthetic vector (kinds as ntt_fill) */
+int ntt_rplan_fill(ntt_rplan* rp, void* d_x, int kind, uint64_t seed, void* hip_stream);
+/* per-launch timing of the row (which = 0) or column (1) transforms, as ntt_plan_last_launch_ms */
+int ntt_rplan_set_profiling(ntt_rplan* rp, int enable);
+int ntt_rplan_last_launch_ms(ntt_rplan* rp, int which, float* ms, unsigned max_launches, unsigned* nlaunches);
+int ntt_rplan_destroy(ntt_rplan* rp);
+
 /* ---------------------------------------------------------------- single-process multi-GPU
  * New (the reference has no multi-GPU code).  One plan drives `ngpus` devices of one node (power of
  * two); a transform is the four-step with ONE RCCL all-to-all over xGMI (ncclCommInitAll over
  * `devices`).  d_data[g] / hip_streams[g] belong to devices[g] (streams may be NULL = default
- * streams); each d_data[g] holds n / ngpus elements.  Layouts (as ntt_amd/distributed.py), with
+ * streams); each d_data[g] holds n / ngpus elements.  Device g runs ntt_rplan rank g.  Layouts (as
+ * ntt_amd/distributed.py), with
  * n1 = 2^ceil(log_n/2), n2 = 2^floor(log_n/2), r = n1/ngpus, c = n2/ngpus:
  *   forward input  (row layout):    d_data[g] = [r][n2], element (a, j2) = x[g r + a + n1 j2]
- *   forward output (column layout): d_data[g] = [c][n1], element (kc, k1) = X[g c + kc + n2 k1]
+ *   forward output (column layout): d_data[g] = [n1][c], element (k1, kc) = X[g c + kc + n2 k1]
  * The inverse takes the column layout back to the row layout (1/n included).  Asynchronous. */
 typedef struct ntt_mplan ntt_mplan;
 int ntt_mplan_create(ntt_mplan** out, int field_id, unsigned log_n, unsigned limbs64, int ngpus, const int* devices);

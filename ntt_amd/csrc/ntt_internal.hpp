@@ -1,0 +1,30 @@
+// Library-internal entry points between translation units (not part of the C ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ntt.h"
+
+namespace ntt {
+
+// Four-step addressing of one local transform (PassArgs::fs and friends, ntt_kernels.hpp).
+struct FsIO {
+  uint32_t fs = 0;                  // FS_MAP_IN | FS_MAP_OUT | FS_IL
+  uint32_t il = 0;                  // Mode I: log2 of the interleave
+  uint32_t map_lc = 0;              // chunk-map shift
+  uint64_t map_ps = 0;              // peer stride (elements)
+  const void* tw_epi = nullptr;     // final-pass twiddle table (plan_build_fs_table) or null
+};
+
+// Transform(s) of `plan` from `in` (+ `in2`: first pass starts from in * in2, polymul inverse) to
+// `out` with the four-step maps.  Mode I: 2^io.il interleaved transforms (batch ignored).
+int plan_run_fs(ntt_plan* plan, const void* in, const void* in2, void* out, unsigned batch, bool inverse,
+                const FsIO& io, hipStream_t st);
+// table[a][b] = w_n^(+-(row0 + a)(col0 + b)) in the plan's epilogue format (n = the plan's size);
+// 2^(log_rows + log_cols) entries of plan_table_entry_bytes() bytes.
+int plan_build_fs_table(ntt_plan* plan, void* table, unsigned log_rows, unsigned log_cols, uint64_t row0,
+                        uint64_t col0, bool inverse, hipStream_t st);
+size_t plan_table_entry_bytes(const ntt_plan* plan);
+int plan_device(const ntt_plan* plan);
+
+}  // namespace ntt

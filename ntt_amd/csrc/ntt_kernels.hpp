@@ -46,7 +46,21 @@ struct PassArgs {
   uint32_t flags;        // bit 0: multiply outputs by ninv (single-pass inverse)
   uint32_t src_user;     // column pass: src is the caller's buffer (E::MEMW words/element), not scratch (E::SCRW)
   size_t batch_stride;   // 32-bit words between batched transforms in the caller's buffers (n * E::MEMW)
+  // ---- distributed four-step addressing (ntt_rplan_*); fs == 0: plain batched transforms.
+  // Mode B (fs & FS_IL == 0): transform b (= blockIdx.y) of a batch; a mapped position p lives at
+  //   (p >> map_lc) * map_ps + (b << map_lc) + (p mod 2^map_lc): the per-peer chunks [G][batch][2^map_lc]
+  //   of an all-to-all (row transforms: packed output of the forward, chunked input of the inverse).
+  // Mode I (fs & FS_IL): 2^il transforms interleaved, element j of transform b at j 2^il + b (the
+  //   [n1][c] column layout); every pass groups T adjacent transforms, so runs stay contiguous.  A
+  //   mapped input index P lives at (P >> map_lc) * map_ps + (P mod 2^map_lc) (peer chunks of r c).
+  uint32_t fs;           // FS_* bits
+  uint32_t il;           // Mode I: log2 of the interleave
+  uint32_t map_lc;
+  uint64_t map_ps;
+  const uint32_t* tw_epi;  // final pass: multiply output k of transform b by this table's entry (w R_e,
+                           // E::SCRW words; index b N + k in Mode B, k 2^il + b in Mode I) or null
 };
+enum : uint32_t { FS_MAP_IN = 1u, FS_MAP_OUT = 2u, FS_IL = 4u };
 
 template <class E, int KIND>
 hipError_t launch_pass_kind(int logr, const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t grid,
@@ -58,6 +72,10 @@ template <class E>
 hipError_t launch_build_tw(uint32_t* out, size_t count, uint32_t log_r, uint32_t log_t, uint32_t log_m,
                            const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits, const typename E::Args& F,
                            hipStream_t st, const uint32_t* clo = nullptr, const uint32_t* chi = nullptr);
+template <class E>
+hipError_t launch_build_fs_tw(uint32_t* out, uint32_t log_rows, uint32_t log_cols, uint64_t row0, uint64_t col0,
+                              uint32_t log_n, const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits,
+                              const typename E::Args& F, hipStream_t st);
 template <class E>
 hipError_t launch_naive(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t batch, hipStream_t st);
 // Fill local element i with the synthetic value of global index

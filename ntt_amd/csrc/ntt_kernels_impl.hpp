@@ -229,7 +229,10 @@ __device__ __forceinline__ void substage(uint32_t (&x)[E::EPT][E::W], uint32_t (
 //              A.tw_in over the in-column index d) and c^col folded into the outer-twiddle table
 //              (PlanImpl::coset).
 enum : int { PRO_NONE = 0, PRO_PW = 1, PRO_COSET = 2 };
-template <class E, int LOGR, int KIND, bool FULLTW, bool FAST, int PRO = PRO_NONE, bool SRC_USER = true>
+// FSM: four-step addressing (PassArgs::fs) compiled in: 0 = plain batched transforms (every
+// product path), 1 = chunk maps / interleave, 2 = the same plus the output twiddle epilogue.
+template <class E, int LOGR, int KIND, bool FULLTW, bool FAST, int PRO = PRO_NONE, bool SRC_USER = true,
+          int FSM = 0>
 __global__ __launch_bounds__((1 << E::TILE_LOG) / E::EPT) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
 void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                               const PassArgs<E> A) {
@@ -249,15 +252,44 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
 
   const int t = threadIdx.x;
   if (t >= NT) return;
-  const size_t bidx = (size_t)blockIdx.y * (A.batch_stride / E::MEMW);  // first element of this transform
-  src += bidx * SW;
-  dst += bidx * DW;
+  // Four-step addressing (PassArgs::fs, ntt_rplan_*): the first pass may read and the last pass may
+  // write through the per-peer chunk maps, and Mode I runs 2^il interleaved transforms.  All flags
+  // are kernel arguments (wave-uniform branches); fs == 0 is the plain batched transform.
+  constexpr bool IN_USER = (KIND == KIND_COLUMN && SRC_USER) || KIND == KIND_SINGLE;
+  constexpr bool EPI = FSM == 2 && KIND != KIND_COLUMN;
+  const bool fs_il = FSM > 0 && (A.fs & FS_IL) != 0;
+  const bool map_in = FSM > 0 && IN_USER && (A.fs & FS_MAP_IN);
+  const bool map_out = FSM > 0 && KIND != KIND_COLUMN && (A.fs & FS_MAP_OUT);
+  const bool single_il = KIND == KIND_SINGLE && fs_il;  // one interleaved transform per workgroup
+  const uint32_t bq = blockIdx.y;
+  const size_t bidx = (size_t)bq * (A.batch_stride / E::MEMW);  // first element of this transform
+  if (!map_in && !single_il) src += bidx * SW;
+  if (!map_out && !single_il) dst += bidx * DW;
   const size_t boff = bidx * E::MEMW;  // caller-buffer words (src2)
+  const size_t mlc = ((size_t)1 << A.map_lc) - 1;
+  // input element `pos` (transform-relative; Mode I column passes: the interleaved linear index)
+  auto in_pos = [&](size_t pos) -> size_t {
+    if (single_il) pos = (pos << A.il) + bq;
+    if (!map_in) return pos;
+    if (fs_il) return (pos >> A.map_lc) * A.map_ps + (pos & mlc);
+    return (pos >> A.map_lc) * A.map_ps + ((size_t)bq << A.map_lc) + (pos & mlc);
+  };
+  // output element (pre-map position as above) -> address; epilogue-table index of the same element
+  auto out_pos = [&](size_t pos) -> size_t {
+    if (single_il) pos = (pos << A.il) + bq;
+    if (!map_out) return pos;
+    return (pos >> A.map_lc) * A.map_ps + ((size_t)bq << A.map_lc) + (pos & mlc);
+  };
+  auto epi_idx = [&](size_t pos) -> size_t {
+    if (single_il) return (pos << A.il) + bq;
+    return fs_il ? pos : (((size_t)bq << A.log_n) + pos);
+  };
 
   // ------------------------------------------------------------------ workgroup geometry
   size_t colbase = 0;  // column pass: first element of this WG's column group
   uint32_t col0 = 0;   // column pass: column index (within block) of local column 0
   uint32_t mid = 0, k10 = 0, midrev = 0;  // final pass
+  uint32_t b0 = 0, tb_log = 0;            // final pass, Mode I: first transform, log2 transforms per WG
   const uint32_t w = blockIdx.x;
   if constexpr (KIND == KIND_COLUMN) {
     const uint32_t log_s = A.log_blk - LOGR;
@@ -268,7 +300,17 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
   } else if constexpr (KIND == KIND_FINAL) {
     const uint32_t w1_log = A.log_n - A.r1 - LOGR;  // W1 = n / (R_1 R_p)
     mid = w & ((1u << w1_log) - 1);
-    k10 = (w >> w1_log) * T;
+    if (fs_il) {
+      // T = (adjacent transforms) x (adjacent k_1 values): as many transforms as the interleave has
+      constexpr uint32_t tl = __builtin_ctz(T);
+      tb_log = tl < A.il ? tl : A.il;
+      const uint32_t tk_log = tl - tb_log;
+      const uint32_t rest = w >> w1_log;
+      k10 = (rest & ((1u << (A.r1 - tk_log)) - 1)) << tk_log;
+      b0 = (rest >> (A.r1 - tk_log)) << tb_log;
+    } else {
+      k10 = (w >> w1_log) * T;
+    }
     uint32_t m = mid;
     for (uint32_t i = 0; i < A.nmid; ++i) {
       const uint32_t d = m & ((1u << A.mid_bits[i]) - 1);
@@ -305,12 +347,18 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
         if constexpr (KIND == KIND_COLUMN) {
           pos = colbase + c + ((size_t)pi << log_s);
         } else if constexpr (KIND == KIND_FINAL) {
-          const size_t beta = ((size_t)(k10 + c) << (A.log_n - A.r1 - LOGR)) + mid;
-          pos = (beta << LOGR) + pi;
+          if (fs_il) {
+            const uint32_t k1 = k10 + (c >> tb_log), b = b0 + (c & ((1u << tb_log) - 1));
+            const size_t beta = ((size_t)k1 << (A.log_n - A.r1 - LOGR)) + mid;
+            pos = (((beta << LOGR) + pi) << A.il) + b;
+          } else {
+            const size_t beta = ((size_t)(k10 + c) << (A.log_n - A.r1 - LOGR)) + mid;
+            pos = (beta << LOGR) + pi;
+          }
         } else {
           pos = pi;
         }
-        E::template load<SW>(x[j * Q + d], src, NTT_NOMEM(pos));
+        E::template load<SW>(x[j * Q + d], src, NTT_NOMEM(IN_USER ? in_pos(pos) : pos));
         if constexpr (PRO == PRO_PW) {
           uint32_t y[E::W];
           E::load(y, A.src2 + boff, pos);
@@ -365,12 +413,17 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
             // contiguous T * R run: HBM-streamed for pass 1, L2-resident later); the Montgomery
             // product removes R_e.  32 B per entry instead of a 80-B Shoup pair.
             uint32_t tw[E::W];
-            E::template load<E::SCRW>(tw, A.tw_full, NTT_NOMEM(((size_t)col0 << LOGR) + (kn * T + c)));
+            size_t ti = ((size_t)col0 << LOGR) + (kn * T + c);
+            if (fs_il) {  // Mode I: transform columns (col0 + c) >> il, in the table's column-group-major layout
+              const uint32_t tc = (col0 + c) >> A.il;
+              ti = ((size_t)(tc & ~(uint32_t)(T - 1)) << LOGR) + kn * T + (tc & (T - 1));
+            }
+            E::template load<E::SCRW>(tw, A.tw_full, NTT_NOMEM(ti));
             E::mulv(v, tw, A.F);
           } else {
             // outer twiddle w_{N_i}^{col * kn} = w_n^{(col * kn) << log_m} from the two-level
             // tables: t = (lo R_e) * hi, then the Montgomery product v * t / R_e = v * lo * hi
-            const size_t e = ((size_t)(col0 + c) * kn) << A.log_m;
+            const size_t e = ((size_t)((col0 + c) >> A.il) * kn) << A.log_m;  // il = 0 unless Mode I
             typename E::Tw tl, th;
             E::tload(tl, A.tw_lo, (uint32_t)(e & ((1u << A.lo_bits) - 1)));
             E::tload(th, A.tw_hi, (uint32_t)(e >> A.lo_bits));
@@ -380,15 +433,33 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
           pos = colbase + c + ((size_t)kn << log_s);
           E::template store_lazy<E::MUL_OUT, FAST, DW>(dst, NTT_NOMEM(pos), v, A.F);  // scratch: < 2p, read by the next pass
         } else if constexpr (KIND == KIND_FINAL) {
-          pos = (size_t)(k10 + c) + ((size_t)midrev << A.r1) + ((size_t)kn << (A.log_n - LOGR));
-          E::template store<E::IN * Q, FAST, DW>(dst, NTT_NOMEM(pos), v, A.F);
+          if (fs_il) {
+            const uint32_t k1 = k10 + (c >> tb_log), b = b0 + (c & ((1u << tb_log) - 1));
+            pos = (((size_t)k1 + ((size_t)midrev << A.r1) + ((size_t)kn << (A.log_n - LOGR))) << A.il) + b;
+          } else {
+            pos = (size_t)(k10 + c) + ((size_t)midrev << A.r1) + ((size_t)kn << (A.log_n - LOGR));
+          }
+          if constexpr (EPI) {  // four-step twiddle w_n^(j1 k2) of this output (ntt_rplan), then the pack map
+            uint32_t tw[E::W];
+            E::template load<E::SCRW>(tw, A.tw_epi, epi_idx(pos));
+            E::mulv(v, tw, A.F);
+            E::template store<E::MUL_OUT, FAST, DW>(dst, NTT_NOMEM(out_pos(pos)), v, A.F);
+          } else {
+            E::template store<E::IN * Q, FAST, DW>(dst, NTT_NOMEM(out_pos(pos)), v, A.F);
+          }
         } else {
           pos = kn;
-          if (A.flags & 1u) {
+          if constexpr (EPI) {
+            if (A.flags & 1u) E::mul(v, A.F.ninv, A.F);
+            uint32_t tw[E::W];
+            E::template load<E::SCRW>(tw, A.tw_epi, epi_idx(pos));
+            E::mulv(v, tw, A.F);
+            E::template store<E::MUL_OUT, FAST>(dst, out_pos(pos), v, A.F);
+          } else if (A.flags & 1u) {
             E::mul(v, A.F.ninv, A.F);
-            E::template store<E::MUL_OUT, FAST>(dst, pos, v, A.F);
+            E::template store<E::MUL_OUT, FAST>(dst, out_pos(pos), v, A.F);
           } else {
-            E::template store<E::IN * Q, FAST>(dst, pos, v, A.F);
+            E::template store<E::IN * Q, FAST>(dst, out_pos(pos), v, A.F);
           }
         }
       });
@@ -459,6 +530,34 @@ hipError_t launch_build_tw(uint32_t* out, size_t count, uint32_t log_r, uint32_t
                            hipStream_t st, const uint32_t* clo, const uint32_t* chi) {
   hipLaunchKernelGGL((k_build_tw<E>), dim3((uint32_t)((count + 255) / 256)), dim3(256), 0, st, out, count, log_r,
                      log_t, log_m, lo, hi, lo_bits, F, clo, chi);
+  return hipGetLastError();
+}
+
+// Four-step twiddle table of one rank (ntt_rplan): entry (a, b) at a 2^log_cols + b holds
+// w_n^((row0 + a)(col0 + b) mod n) R_e (the epilogue of the final pass multiplies by it with mulv),
+// from the two-level tables (lo_s = lo R_e, so lo_s * hi = w R_e).
+template <class E>
+__global__ void k_build_fs_tw(uint32_t* __restrict__ out, uint32_t log_rows, uint32_t log_cols, uint64_t row0,
+                              uint64_t col0, uint32_t log_n, const uint32_t* __restrict__ lo,
+                              const uint32_t* __restrict__ hi, uint32_t lo_bits, const typename E::Args F) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >> (log_rows + log_cols)) return;
+  const uint64_t a = idx >> log_cols, b = idx & ((1ull << log_cols) - 1);
+  const uint64_t e = ((row0 + a) * (col0 + b)) & ((1ull << log_n) - 1);
+  typename E::Tw x, y;
+  E::tload(x, lo, (uint32_t)(e & ((1ull << lo_bits) - 1)));
+  E::tload(y, hi, (uint32_t)(e >> lo_bits));
+  E::mul(x.w, y, F);
+  E::template store<E::MUL_OUT, false, E::SCRW>(out, idx, x.w, F);
+}
+
+template <class E>
+hipError_t launch_build_fs_tw(uint32_t* out, uint32_t log_rows, uint32_t log_cols, uint64_t row0, uint64_t col0,
+                              uint32_t log_n, const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits,
+                              const typename E::Args& F, hipStream_t st) {
+  const size_t count = 1ull << (log_rows + log_cols);
+  hipLaunchKernelGGL((k_build_fs_tw<E>), dim3((uint32_t)((count + 255) / 256)), dim3(256), 0, st, out, log_rows,
+                     log_cols, row0, col0, log_n, lo, hi, lo_bits, F);
   return hipGetLastError();
 }
 
@@ -697,17 +796,29 @@ hipError_t launch_count_noncanonical(const uint32_t* d, size_t n, const ModWords
 // transforms 3 <= r <= tile_log.  Only those are instantiated.
 // Plain (no prologue) pass launch; later column passes of engines whose scratch is narrower than the
 // caller's layout read scratch (SRC_USER = false).
-template <class E, int LOGR, int KIND, bool FULLTW, bool FAST>
+template <class E, int LOGR, int KIND, bool FULLTW, bool FAST, int FSM>
 static hipError_t launch_plain(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, dim3 g, dim3 b,
                                hipStream_t st) {
   if constexpr (KIND == KIND_COLUMN && E::SCRW != E::MEMW) {
     if (!A.src_user) {
-      hipLaunchKernelGGL((k_pass<E, LOGR, KIND, FULLTW, FAST, PRO_NONE, false>), g, b, 0, st, src, dst, A);
+      hipLaunchKernelGGL((k_pass<E, LOGR, KIND, FULLTW, FAST, PRO_NONE, false, FSM>), g, b, 0, st, src, dst, A);
       return hipGetLastError();
     }
   }
-  hipLaunchKernelGGL((k_pass<E, LOGR, KIND, FULLTW, FAST>), g, b, 0, st, src, dst, A);
+  hipLaunchKernelGGL((k_pass<E, LOGR, KIND, FULLTW, FAST, PRO_NONE, true, FSM>), g, b, 0, st, src, dst, A);
   return hipGetLastError();
+}
+
+// FSM (four-step addressing) instance for this pass: column passes need it only for a mapped input
+// (first pass) or Mode I twiddles; final / single passes for a mapped output, Mode I or the epilogue.
+template <class E, int KIND, int LOGR, bool FULLTW, bool FAST>
+static hipError_t launch_fsm(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, dim3 g, dim3 b,
+                             hipStream_t st) {
+  if (A.fs == 0 && !A.tw_epi) return launch_plain<E, LOGR, KIND, FULLTW, FAST, 0>(src, dst, A, g, b, st);
+  if constexpr (KIND != KIND_COLUMN) {
+    if (A.tw_epi) return launch_plain<E, LOGR, KIND, FULLTW, FAST, 2>(src, dst, A, g, b, st);
+  }
+  return launch_plain<E, LOGR, KIND, FULLTW, FAST, 1>(src, dst, A, g, b, st);
 }
 
 template <class E, int KIND, int LOGR>
@@ -725,24 +836,28 @@ static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassAr
       if (A.F.red_ok) {
         if constexpr (KIND == KIND_COLUMN) {
           if (A.tw_full && A.src2) {
-            hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true, true, PRO_PW>), g, b, 0, st, src, dst, A);
+            if (A.fs)  // Mode I polymul inverse (ntt_rplan)
+              hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true, true, PRO_PW, true, 1>), g, b, 0, st, src, dst, A);
+            else
+              hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true, true, PRO_PW>), g, b, 0, st, src, dst, A);
             return hipGetLastError();
           }
           if (A.tw_full && A.tw_in) {
+            if (A.fs) return hipErrorInvalidValue;
             hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true, true, PRO_COSET>), g, b, 0, st, src, dst, A);
             return hipGetLastError();
           }
-          if (A.tw_full) return launch_plain<E, LOGR, KIND, true, true>(src, dst, A, g, b, st);
+          if (A.tw_full) return launch_fsm<E, KIND, LOGR, true, true>(src, dst, A, g, b, st);
         }
         if (A.src2 || A.tw_in) return hipErrorInvalidValue;  // fused prologues: FAST column + full tables
-        return launch_plain<E, LOGR, KIND, false, true>(src, dst, A, g, b, st);
+        return launch_fsm<E, KIND, LOGR, false, true>(src, dst, A, g, b, st);
       }
     }
     if (A.src2 || A.tw_in) return hipErrorInvalidValue;
     if constexpr (KIND == KIND_COLUMN) {
-      if (A.tw_full) return launch_plain<E, LOGR, KIND, true, false>(src, dst, A, g, b, st);
+      if (A.tw_full) return launch_fsm<E, KIND, LOGR, true, false>(src, dst, A, g, b, st);
     }
-    return launch_plain<E, LOGR, KIND, false, false>(src, dst, A, g, b, st);
+    return launch_fsm<E, KIND, LOGR, false, false>(src, dst, A, g, b, st);
   }
 }
 
@@ -827,6 +942,9 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
   template hipError_t launch_build_tw<E>(uint32_t*, size_t, uint32_t, uint32_t, uint32_t, const uint32_t*,        \
                                          const uint32_t*, uint32_t, const typename E::Args&, hipStream_t,          \
                                          const uint32_t*, const uint32_t*);                                        \
+  template hipError_t launch_build_fs_tw<E>(uint32_t*, uint32_t, uint32_t, uint64_t, uint64_t, uint32_t,           \
+                                            const uint32_t*, const uint32_t*, uint32_t, const typename E::Args&,    \
+                                            hipStream_t);                                                           \
   template hipError_t launch_scale_pow<E>(uint32_t*, uint32_t, uint32_t, const uint32_t*, const uint32_t*, uint32_t, \
                                           const typename E::Args&, hipStream_t);                                   \
   template hipError_t launch_count_noncanonical<E>(const uint32_t*, size_t, const ModWords<E::MEMW>&,              \

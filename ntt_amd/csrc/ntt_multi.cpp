@@ -5,11 +5,12 @@
 // schedule): n = n1 n2, n1 = 2^ceil(L/2), n2 = 2^floor(L/2), r = n1 / G rows and c = n2 / G
 // columns per device.
 //   input  (row layout):    device g holds [r][n2], element (a, j2) = x[g r + a + n1 j2]
-//   output (column layout): device g holds [c][n1], element (kc, k1) = X[g c + kc + n2 k1]
-// Forward on every device: batched n2-point NTTs of its rows -> twiddle w_n^(j1 k2) fused with the
-// pack into per-peer chunks -> all-to-all (RCCL, grouped over the devices) -> local transpose ->
-// batched n1-point NTTs.  The inverse mirrors it (column layout in, row layout out).  All work is
-// asynchronous on the callers' per-device streams.  The reference has no multi-GPU code.
+//   output (column layout): device g holds [n1][c], element (k1, kc) = X[g c + kc + n2 k1]
+// Forward on every device (its ntt_rplan, ntt_rplan.cpp): batched n2-point NTTs of its rows whose
+// last pass applies w_n^(j1 k2) and stores straight into the per-peer chunks -> all-to-all (RCCL,
+// grouped over the devices) -> interleaved n1-point NTTs reading the chunks as they arrived.  The
+// inverse mirrors it (column layout in, row layout out).  All work is asynchronous on the callers'
+// per-device streams.  The reference has no multi-GPU code.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -66,26 +67,22 @@ struct ntt_mplan {
   unsigned log_n = 0, log_g = 0, log_n1 = 0, log_n2 = 0, log_r = 0, log_c = 0;
   unsigned elem_bytes = 0;
   std::vector<int> dev;
-  std::vector<ntt_plan*> rows, cols, tw;
-  std::vector<void*> send, recv;
-  std::vector<void*> send2, recv2;  // 2 local_n each: the polymul's batched (a, b) exchange, on first use
+  std::vector<ntt_rplan*> rp;       // device g's local steps (ntt_rplan.cpp)
+  std::vector<void*> send, recv;    // [G][chunk] per device
+  std::vector<void*> send2, recv2;  // [G][2][chunk]: the polymul's batched (a, b) exchange, on first use
   std::vector<ncclComm_t> comm;
 
   ~ntt_mplan() {
     int cur = 0;
-    hipGetDevice(&cur);
+    (void)hipGetDevice(&cur);
     for (size_t g = 0; g < dev.size(); ++g) {
-      hipSetDevice(dev[g]);
+      (void)hipSetDevice(dev[g]);
       if (g < comm.size() && comm[g]) rccl().CommDestroy(comm[g]);
-      if (g < send.size() && send[g]) hipFree(send[g]);
-      if (g < recv.size() && recv[g]) hipFree(recv[g]);
-      if (g < send2.size() && send2[g]) hipFree(send2[g]);
-      if (g < recv2.size() && recv2[g]) hipFree(recv2[g]);
-      if (g < cols.size() && cols[g] && cols[g] != rows[g]) ntt_plan_destroy(cols[g]);
-      if (g < rows.size() && rows[g]) ntt_plan_destroy(rows[g]);
-      if (g < tw.size() && tw[g]) ntt_plan_destroy(tw[g]);
+      for (auto* v : {&send, &recv, &send2, &recv2})
+        if (g < v->size() && (*v)[g]) (void)hipFree((*v)[g]);
+      if (g < rp.size() && rp[g]) ntt_rplan_destroy(rp[g]);
     }
-    hipSetDevice(cur);
+    (void)hipSetDevice(cur);
   }
   size_t local_n() const { return 1ull << (log_n - log_g); }
   hipStream_t stream(void* const* streams, int g) const {
@@ -147,10 +144,19 @@ size_t chunk_words(const ntt_mplan* m) {  // per-peer chunk of one vector: r * c
 // free or reuse them.
 int drain(ntt_mplan* m, void* const* streams, int rc) {
   for (int g = 0; g < m->ngpus; ++g) {
-    hipSetDevice(m->dev[g]);
-    hipStreamSynchronize(m->stream(streams, g));
+    (void)hipSetDevice(m->dev[g]);
+    (void)hipStreamSynchronize(m->stream(streams, g));
   }
   return rc;
+}
+
+int alloc_pair(std::vector<void*>& v, int g, size_t bytes) {
+  if (v[g]) return NTT_OK;
+  if (hipMalloc(&v[g], bytes) != hipSuccess) {
+    v[g] = nullptr;
+    return NTT_ERR_HIP;
+  }
+  return NTT_OK;
 }
 
 int ensure_pair_buffers(ntt_mplan* m) {
@@ -159,75 +165,39 @@ int ensure_pair_buffers(ntt_mplan* m) {
     m->recv2.assign(m->ngpus, nullptr);
   }
   for (int g = 0; g < m->ngpus; ++g) {
-    if (m->send2[g]) continue;
-    hipSetDevice(m->dev[g]);
-    if (hipMalloc(&m->send2[g], 2 * m->local_n() * m->elem_bytes) != hipSuccess) {
-      m->send2[g] = nullptr;
-      return NTT_ERR_HIP;
-    }
-    if (hipMalloc(&m->recv2[g], 2 * m->local_n() * m->elem_bytes) != hipSuccess) {
-      hipFree(m->send2[g]);
-      m->send2[g] = nullptr;
-      return NTT_ERR_HIP;
-    }
+    (void)hipSetDevice(m->dev[g]);
+    if (int rc = alloc_pair(m->send2, g, 2 * m->local_n() * m->elem_bytes)) return rc;
+    if (int rc = alloc_pair(m->recv2, g, 2 * m->local_n() * m->elem_bytes)) return rc;
   }
   return NTT_OK;
 }
 
-// Forward of several vectors in row layout to column layout with ONE exchange: v[k][g] is vector k's
+// Forward of nv vectors in row layout to column layout with ONE exchange: v[k][g] is vector k's
 // share on device g; the per-peer chunks of all vectors travel together ([G][nv][chunk]).
 int forward_vectors(ntt_mplan* m, void* const* const* v, int nv, void* const* streams) {
-  const uint64_t r = 1ull << m->log_r, chunk = 1ull << (m->log_r + m->log_c);
   const std::vector<void*>& sb = nv == 1 ? m->send : m->send2;
   const std::vector<void*>& rb = nv == 1 ? m->recv : m->recv2;
-  for (int g = 0; g < m->ngpus; ++g) {
-    hipSetDevice(m->dev[g]);
-    void* s = m->stream(streams, g);
-    for (int k = 0; k < nv; ++k) {
-      if (int rc = ntt_forward_batch(m->rows[g], v[k][g], (unsigned)r, s)) return rc;
-      if (int rc = ntt_twiddle_pack_ex(m->tw[g], v[k][g], static_cast<char*>(sb[g]) + k * chunk * m->elem_bytes,
-                                       m->log_r, m->log_n2, m->log_c, (uint64_t)g * r, 0, nv * chunk, s))
+  for (int g = 0; g < m->ngpus; ++g)
+    for (int k = 0; k < nv; ++k)
+      if (int rc = ntt_rplan_forward_rows(m->rp[g], v[k][g], sb[g], (unsigned)nv, (unsigned)k, m->stream(streams, g)))
         return rc;
-    }
-  }
   if (int rc = exchange(m, sb, rb, nv * chunk_words(m), streams)) return rc;
-  for (int g = 0; g < m->ngpus; ++g) {
-    hipSetDevice(m->dev[g]);
-    void* s = m->stream(streams, g);
-    for (int k = 0; k < nv; ++k) {
-      // recv = [G][nv][r][c]: vector k's rows g' r .. (g'+1) r - 1 at (g' nv + k) chunk -> [c][n1]
-      if (int rc = ntt_transpose_ex(m->tw[g], static_cast<const char*>(rb[g]) + k * chunk * m->elem_bytes, v[k][g],
-                                    m->log_n1, m->log_c, m->log_r, nv * chunk, s))
+  for (int g = 0; g < m->ngpus; ++g)
+    for (int k = 0; k < nv; ++k)
+      if (int rc = ntt_rplan_forward_cols(m->rp[g], rb[g], v[k][g], (unsigned)nv, (unsigned)k, m->stream(streams, g)))
         return rc;
-      if (int rc = ntt_forward_batch(m->cols[g], v[k][g], 1u << m->log_c, s)) return rc;
-    }
-  }
   return NTT_OK;
 }
 
-// Inverse from column layout to row layout.  With `b` (polymul) the first column pass starts from
-// the pointwise product a * b (ntt_inverse_pointwise_batch) and the result lands in `out`.
+// Inverse from column layout to row layout; with b (polymul) the first column pass starts from the
+// pointwise product a * b and the result lands in `out`.
 int inverse_vector(ntt_mplan* m, void* const* a, void* const* b, void* const* out, void* const* streams) {
-  const uint64_t c = 1ull << m->log_c;
-  for (int g = 0; g < m->ngpus; ++g) {
-    hipSetDevice(m->dev[g]);
-    void* s = m->stream(streams, g);
-    if (b) {
-      if (int rc = ntt_inverse_pointwise_batch(m->cols[g], a[g], b[g], out[g], (unsigned)c, s)) return rc;
-    } else if (int rc = ntt_inverse_batch(m->cols[g], out[g], (unsigned)c, s)) {
+  for (int g = 0; g < m->ngpus; ++g)
+    if (int rc = ntt_rplan_inverse_cols(m->rp[g], a[g], b ? b[g] : nullptr, m->send[g], m->stream(streams, g)))
       return rc;
-    }
-    if (int rc = ntt_twiddle_pack(m->tw[g], out[g], m->send[g], m->log_c, m->log_n1, m->log_r, (uint64_t)g * c, 1, s))
-      return rc;
-  }
   if (int rc = exchange(m, m->send, m->recv, chunk_words(m), streams)) return rc;
-  for (int g = 0; g < m->ngpus; ++g) {
-    hipSetDevice(m->dev[g]);
-    void* s = m->stream(streams, g);
-    // recv = [G][c][r] = [n2][r] -> [r][n2]
-    if (int rc = ntt_transpose(m->tw[g], m->recv[g], out[g], m->log_n2, m->log_r, s)) return rc;
-    if (int rc = ntt_inverse_batch(m->rows[g], out[g], 1u << m->log_r, s)) return rc;
-  }
+  for (int g = 0; g < m->ngpus; ++g)
+    if (int rc = ntt_rplan_inverse_rows(m->rp[g], m->recv[g], out[g], m->stream(streams, g))) return rc;
   return NTT_OK;
 }
 
@@ -248,24 +218,20 @@ int ntt_mplan_create(ntt_mplan** out, int field_id, unsigned log_n, unsigned lim
   if (m->log_g > m->log_n2) { delete m; return NTT_ERR_ARG; }
   m->log_r = m->log_n1 - m->log_g;
   m->log_c = m->log_n2 - m->log_g;
-  m->elem_bytes = 8 * limbs64;
   m->dev.assign(devices, devices + ngpus);
-  m->rows.assign(ngpus, nullptr);
-  m->cols.assign(ngpus, nullptr);
-  m->tw.assign(ngpus, nullptr);
+  m->rp.assign(ngpus, nullptr);
   m->send.assign(ngpus, nullptr);
   m->recv.assign(ngpus, nullptr);
   int rc = NTT_OK;
   for (int g = 0; g < ngpus && rc == NTT_OK; ++g) {
     if (hipSetDevice(devices[g]) != hipSuccess) { rc = NTT_ERR_HIP; break; }
-    rc = ntt_plan_create(&m->rows[g], field_id, m->log_n2, limbs64, devices[g]);
-    if (rc == NTT_OK)
-      rc = (m->log_n1 == m->log_n2) ? (m->cols[g] = m->rows[g], NTT_OK)
-                                    : ntt_plan_create(&m->cols[g], field_id, m->log_n1, limbs64, devices[g]);
-    if (rc == NTT_OK) rc = ntt_plan_create_ex(&m->tw[g], field_id, log_n, limbs64, devices[g], NTT_PLAN_TWIDDLE_ONLY);
-    if (rc == NTT_OK && (hipMalloc(&m->send[g], m->local_n() * m->elem_bytes) != hipSuccess ||
-                         hipMalloc(&m->recv[g], m->local_n() * m->elem_bytes) != hipSuccess))
-      rc = NTT_ERR_HIP;
+    rc = ntt_rplan_create(&m->rp[g], field_id, log_n, limbs64, ngpus, g, devices[g]);
+    if (rc == NTT_OK) {
+      unsigned eb = 0;
+      ntt_rplan_info(m->rp[g], nullptr, nullptr, nullptr, nullptr, &eb);
+      m->elem_bytes = eb;
+      if (alloc_pair(m->send, g, m->local_n() * eb) || alloc_pair(m->recv, g, m->local_n() * eb)) rc = NTT_ERR_HIP;
+    }
   }
   if (rc == NTT_OK) {
     m->comm.assign(ngpus, nullptr);
@@ -290,7 +256,7 @@ int ntt_forward_multi(ntt_mplan* m, void* const* d_data, void* const* streams) {
 int ntt_inverse_multi(ntt_mplan* m, void* const* d_data, void* const* streams) {
   if (!m || !d_data) return NTT_ERR_ARG;
   DeviceGuard guard;
-  const int rc = inverse_vector(m, nullptr, nullptr, d_data, streams);
+  const int rc = inverse_vector(m, d_data, nullptr, d_data, streams);
   return rc ? drain(m, streams, rc) : NTT_OK;
 }
 
@@ -310,11 +276,8 @@ int ntt_mplan_fill(ntt_mplan* m, void* const* d_data, int kind, uint64_t seed, v
   if (!m || !d_data) return NTT_ERR_ARG;
   DeviceGuard guard;
   for (int g = 0; g < m->ngpus; ++g) {
-    hipSetDevice(m->dev[g]);
-    // local element i = (a, j2) -> global row g r + a, column j2: j = g r + a + n1 j2
-    if (int rc = ntt_fill_map(m->tw[g], d_data[g], m->local_n(), kind, seed, (uint64_t)g << m->log_r, m->log_n2,
-                              m->log_n1, m->stream(streams, g)))
-      return rc;
+    (void)hipSetDevice(m->dev[g]);
+    if (int rc = ntt_rplan_fill(m->rp[g], d_data[g], kind, seed, m->stream(streams, g))) return rc;
   }
   return NTT_OK;
 }

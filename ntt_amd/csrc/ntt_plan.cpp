@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "../../include/ntt.h"
+#include "ntt_internal.hpp"
 #include "ntt_kernels.hpp"
 
 using namespace ntt;
@@ -91,6 +92,11 @@ struct PlanBase {
   virtual int transpose(const void* src, void* dst, unsigned log_rows, unsigned log_cols, unsigned log_blk_rows,
                         uint64_t blk_stride, hipStream_t st) = 0;
   virtual int inverse_pointwise(const void* a, const void* b, void* c, unsigned batch, hipStream_t st) = 0;
+  virtual int run_fs(const void* in, const void* in2, void* out, unsigned batch, bool inverse, const ntt::FsIO& io,
+                     hipStream_t st) = 0;
+  virtual int build_fs_table(void* table, unsigned log_rows, unsigned log_cols, uint64_t row0, uint64_t col0,
+                             bool inverse, hipStream_t st) = 0;
+  virtual size_t table_entry_bytes() const = 0;
   virtual int coset(void* d, const uint64_t* shift, unsigned limbs64, bool inverse, hipStream_t st) = 0;
   virtual int count_noncanonical(const void* d, uint64_t count, uint64_t* bad, hipStream_t st) = 0;
   uint64_t n = 0;
@@ -674,7 +680,16 @@ struct PlanImpl final : PlanBase {
   // Fused coset forward: full0 replaces the first pass's outer-twiddle table and tw_in scales its
   // inputs (PRO_COSET in ntt_kernels_impl.hpp).
   int run_io(const uint32_t* in, const uint32_t* in2, uint32_t* out, unsigned batch, bool inverse, hipStream_t st,
-             const uint32_t* full0 = nullptr, const uint32_t* tw_in = nullptr) {
+             const uint32_t* full0 = nullptr, const uint32_t* tw_in = nullptr, const FsIO* io = nullptr) {
+    const uint32_t il = (io && (io->fs & FS_IL)) ? io->il : 0u;
+    auto set_fs = [&](PassArgs<E>& A, uint32_t bits) {
+      if (!io) return;
+      A.fs = io->fs & (bits | FS_IL);
+      A.il = il;
+      A.map_lc = io->map_lc;
+      A.map_ps = io->map_ps;
+    };
+    if (io && (log_n == 0 || npass == 0)) return NTT_ERR_ARG;  // four-step pieces are >= 8 points
     if (log_n == 0) {
       if (out != in) hipMemcpyAsync(out, in, (size_t)batch * MEMW * 4, hipMemcpyDeviceToDevice, st);
       return NTT_OK;
@@ -692,11 +707,14 @@ struct PlanImpl final : PlanBase {
       PassArgs<E> A = base_args(inverse);
       A.tw_int = d_tab + off_int[0];
       A.flags = inverse ? 1u : 0u;
-      e = launch_pass<E>(KIND_SINGLE, (int)r[0], in, out, A, 1, batch, st);
+      set_fs(A, FS_MAP_IN | FS_MAP_OUT);
+      if (io) A.tw_epi = static_cast<const uint32_t*>(io->tw_epi);
+      e = launch_pass<E>(KIND_SINGLE, (int)r[0], in, out, A, 1, il ? (1u << il) : batch, st);
       mark(st);
     } else {
-      if (int rc = ensure_scratch(batch)) return rc;
-      const uint32_t grid = (uint32_t)(n >> tile_log_of<E>());
+      if (il) batch = 1;  // Mode I: the 2^il interleaved transforms are one long column sweep
+      if (int rc = ensure_scratch(il ? (1u << il) : batch)) return rc;
+      const uint32_t grid = (uint32_t)((n << il) >> tile_log_of<E>());
       unsigned blk = log_n;
       for (unsigned i = 0; i + 1 < npass && e == hipSuccess; ++i) {
         PassArgs<E> A = base_args(inverse);
@@ -714,9 +732,10 @@ struct PlanImpl final : PlanBase {
           A.tw_in = tw_in;
           A.tw_full = full0;
         }
-        A.log_blk = blk;
+        A.log_blk = blk + il;
         A.log_m = log_n - blk;
         A.src_user = (i == 0) ? 1u : 0u;
+        set_fs(A, i == 0 ? FS_MAP_IN : 0u);
         const uint32_t* src = (i == 0) ? in : d_scratch;
         e = launch_pass<E>(KIND_COLUMN, (int)r[i], src, d_scratch, A, grid, batch, st);
         mark(st);
@@ -735,12 +754,44 @@ struct PlanImpl final : PlanBase {
           for (unsigned j = 1; j < idx; ++j) off += r[j];
           A.mid_off[m] = off;
         }
+        set_fs(A, FS_MAP_OUT);
+        if (io) A.tw_epi = static_cast<const uint32_t*>(io->tw_epi);
         e = launch_pass<E>(KIND_FINAL, (int)r[npass - 1], d_scratch, out, A, grid, batch, st);
         mark(st);
       }
     }
     return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
   }
+
+  // ---- distributed four-step pieces (ntt_rplan, ntt_amd/csrc/ntt_rplan.cpp)
+  int run_fs(const void* in, const void* in2, void* out, unsigned batch, bool inverse, const FsIO& io,
+             hipStream_t st) override {
+    if (!in || !out || batch == 0 || (flags & NTT_PLAN_TWIDDLE_ONLY)) return NTT_ERR_ARG;
+    auto pin = static_cast<const uint32_t*>(in);
+    auto pout = static_cast<uint32_t*>(out);
+    if (!in2) return run_io(pin, nullptr, pout, batch, inverse, st, nullptr, nullptr, &io);
+    if (!inverse || (io.fs & FS_MAP_IN)) return NTT_ERR_ARG;  // the product is taken at the inverse's load
+    const size_t count = (size_t)n * ((io.fs & FS_IL) ? (1ull << io.il) : batch);
+    if (polymul_fusable() && npass >= 2) {
+      if (int rc = ensure_polymul_table()) return rc;
+      return run_io(pin, static_cast<const uint32_t*>(in2), pout, batch, true, st, nullptr, nullptr, &io);
+    }
+    if (int rc = pointwise_n(pin, static_cast<const uint32_t*>(in2), pout, count, st)) return rc;
+    return run_io(pout, nullptr, pout, batch, true, st, nullptr, nullptr, &io);
+  }
+
+  int build_fs_table(void* table, unsigned log_rows, unsigned log_cols, uint64_t row0, uint64_t col0, bool inverse,
+                     hipStream_t st) override {
+    if (!table || log_rows + log_cols > 40) return NTT_ERR_ARG;
+    const uint32_t* lo = d_tab + (inverse ? off_los_i : off_los_f);
+    const uint32_t* hi = d_tab + (inverse ? off_hi_i : off_hi_f);
+    return launch_build_fs_tw<E>(static_cast<uint32_t*>(table), log_rows, log_cols, row0, col0, log_n, lo, hi,
+                                 lo_bits, inverse ? Fi : Ff, st) == hipSuccess
+               ? NTT_OK
+               : NTT_ERR_HIP;
+  }
+
+  size_t table_entry_bytes() const override { return (size_t)SCRW * 4; }
 
   // Fused polymul is available for multi-pass FAST plans with full outer-twiddle tables.
   bool polymul_fusable() const {
@@ -1155,3 +1206,19 @@ int NTT_GZKP_256(uint32_t* data, uint32_t len, const void* /*reverse*/, uint32_t
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- library-internal (ntt_internal.hpp)
+namespace ntt {
+int plan_run_fs(ntt_plan* plan, const void* in, const void* in2, void* out, unsigned batch, bool inverse,
+                const FsIO& io, hipStream_t st) {
+  if (!plan || !plan->impl) return NTT_ERR_ARG;
+  return plan->impl->run_fs(in, in2, out, batch, inverse, io, st);
+}
+int plan_build_fs_table(ntt_plan* plan, void* table, unsigned log_rows, unsigned log_cols, uint64_t row0,
+                        uint64_t col0, bool inverse, hipStream_t st) {
+  if (!plan || !plan->impl) return NTT_ERR_ARG;
+  return plan->impl->build_fs_table(table, log_rows, log_cols, row0, col0, inverse, st);
+}
+size_t plan_table_entry_bytes(const ntt_plan* plan) { return plan && plan->impl ? plan->impl->table_entry_bytes() : 0; }
+int plan_device(const ntt_plan* plan) { return plan && plan->impl ? plan->impl->device : -1; }
+}  // namespace ntt

@@ -1,0 +1,199 @@
+// One rank of the distributed four-step NTT: the local steps around the all-to-all,
+// fused so that no separate twiddle, pack or transpose pass touches HBM.
+//
+//   n = n1 n2, n1 = 2^ceil(L/2), n2 = 2^floor(L/2); rank g of G owns r = n1/G rows and c = n2/G
+//   columns.  Layouts (ntt.h):
+//     row layout     [r][n2]: local (a, j2)  = x[g r + a + n1 j2]
+//     column layout  [n1][c]: local (k1, kc) = X[g c + kc + n2 k1]   (transform index fastest)
+//
+//   forward rows  : r length-n2 transforms of the row layout; the last pass multiplies output k2 of
+//                   row a by w_n^((g r + a) k2) (per-rank table) and stores it straight into the
+//                   send buffer's peer chunk k2 / c at [a][k2 mod c]                   (Mode B out)
+//   exchange      : the caller's all-to-all of equal chunks; recv = [G][r][c] = [n1][c]
+//   forward cols  : c interleaved length-n1 transforms read recv as it arrived (Mode I) -> x
+//   inverse cols  : c interleaved inverse transforms of x (optionally of x * y: polymul, the
+//                   product taken at the first pass's load); the last pass multiplies by
+//                   w_n^-(j1 (g c + kc)) and writes send = [n1][c], whose peer chunks are contiguous
+//   inverse rows  : r inverse length-n2 transforms reading recv = [G][c][r... ] through the chunk map
+//                   (Mode B in) -> row layout
+// The buffers are the caller's ([G][nvec][r c] elements each), so the exchange can be RCCL through
+// torch.distributed, ncclAllToAll in ntt_mplan, or device copies between virtual ranks.
+#include <hip/hip_runtime.h>
+
+#include "../../include/ntt.h"
+#include "ntt_internal.hpp"
+#include "ntt_kernels.hpp"
+
+using namespace ntt;
+
+struct ntt_rplan {
+  int world = 1, rank = 0, device = 0;
+  unsigned log_n = 0, log_n1 = 0, log_n2 = 0, log_g = 0, log_r = 0, log_c = 0;
+  size_t elem_bytes = 0;
+  ntt_plan *rows = nullptr, *cols = nullptr, *tw = nullptr;
+  void* tab_fwd = nullptr;  // [r][n2]: w_n^((g r + a) k2)
+  void* tab_inv = nullptr;  // [n1][c]: w_n^-(j1 (g c + kc))
+  ~ntt_rplan() {
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(device);
+    if (tab_fwd) (void)hipFree(tab_fwd);
+    if (tab_inv) (void)hipFree(tab_inv);
+    if (rows) ntt_plan_destroy(rows);
+    if (cols) ntt_plan_destroy(cols);
+    if (tw) ntt_plan_destroy(tw);
+    (void)hipSetDevice(cur);
+  }
+  uint64_t chunk() const { return 1ull << (log_r + log_c); }
+};
+
+namespace {
+
+struct DeviceScope {
+  int cur = 0;
+  bool moved = false;
+  explicit DeviceScope(int dev) {
+    (void)hipGetDevice(&cur);
+    if (cur != dev) moved = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceScope() {
+    if (moved) (void)hipSetDevice(cur);
+  }
+};
+
+hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
+
+bool nvec_ok(unsigned nvec, unsigned slot) { return (nvec == 1 || nvec == 2) && slot < nvec; }
+
+}  // namespace
+
+extern "C" {
+
+int ntt_rplan_create(ntt_rplan** out, int field_id, unsigned log_n, unsigned limbs64, int world, int rank,
+                     int device) {
+  if (!out) return NTT_ERR_ARG;
+  *out = nullptr;
+  if (world < 1 || (world & (world - 1)) || rank < 0 || rank >= world || log_n > 40) return NTT_ERR_ARG;
+  auto rp = new ntt_rplan();
+  rp->world = world;
+  rp->rank = rank;
+  rp->device = device;
+  rp->log_n = log_n;
+  rp->log_g = (unsigned)__builtin_ctz((unsigned)world);
+  rp->log_n1 = (log_n + 1) / 2;
+  rp->log_n2 = log_n / 2;
+  // every local transform has >= 8 points (one or more pass kernels) and >= 1 row / column per rank
+  if (rp->log_n2 < 3 || rp->log_g > rp->log_n2) {
+    delete rp;
+    return NTT_ERR_ARG;
+  }
+  rp->log_r = rp->log_n1 - rp->log_g;
+  rp->log_c = rp->log_n2 - rp->log_g;
+  DeviceScope scope(device);
+  int rc = ntt_plan_create(&rp->rows, field_id, rp->log_n2, limbs64, device);
+  if (rc == NTT_OK) rc = ntt_plan_create(&rp->cols, field_id, rp->log_n1, limbs64, device);
+  if (rc == NTT_OK) rc = ntt_plan_create_ex(&rp->tw, field_id, log_n, limbs64, device, NTT_PLAN_TWIDDLE_ONLY);
+  if (rc == NTT_OK) {
+    uint64_t n = 0;
+    unsigned eb = 0;
+    ntt_plan_info(rp->rows, &n, &eb, nullptr, nullptr);
+    rp->elem_bytes = eb;
+    const size_t tb = plan_table_entry_bytes(rp->tw);
+    const size_t local = 1ull << (log_n - rp->log_g);
+    if (hipMalloc(&rp->tab_fwd, local * tb) != hipSuccess || hipMalloc(&rp->tab_inv, local * tb) != hipSuccess)
+      rc = NTT_ERR_HIP;
+  }
+  if (rc == NTT_OK) {
+    const uint64_t g = (uint64_t)rank;
+    rc = plan_build_fs_table(rp->tw, rp->tab_fwd, rp->log_r, rp->log_n2, g << rp->log_r, 0, false, nullptr);
+    if (rc == NTT_OK)
+      rc = plan_build_fs_table(rp->tw, rp->tab_inv, rp->log_n1, rp->log_c, 0, g << rp->log_c, true, nullptr);
+    if (rc == NTT_OK && hipDeviceSynchronize() != hipSuccess) rc = NTT_ERR_HIP;
+  }
+  if (rc != NTT_OK) {
+    delete rp;
+    return rc;
+  }
+  *out = rp;
+  return NTT_OK;
+}
+
+int ntt_rplan_info(const ntt_rplan* rp, uint64_t* local_n, uint64_t* chunk, unsigned* log_n1, unsigned* log_n2,
+                   unsigned* elem_bytes) {
+  if (!rp) return NTT_ERR_ARG;
+  if (local_n) *local_n = 1ull << (rp->log_n - rp->log_g);
+  if (chunk) *chunk = rp->chunk();
+  if (log_n1) *log_n1 = rp->log_n1;
+  if (log_n2) *log_n2 = rp->log_n2;
+  if (elem_bytes) *elem_bytes = (unsigned)rp->elem_bytes;
+  return NTT_OK;
+}
+
+int ntt_rplan_forward_rows(ntt_rplan* rp, const void* d_x, void* d_send, unsigned nvec, unsigned slot, void* s) {
+  if (!rp || !d_x || !d_send || !nvec_ok(nvec, slot)) return NTT_ERR_ARG;
+  DeviceScope scope(rp->device);
+  FsIO io;
+  io.fs = FS_MAP_OUT;
+  io.map_lc = rp->log_c;
+  io.map_ps = nvec * rp->chunk();
+  io.tw_epi = rp->tab_fwd;
+  void* dst = static_cast<char*>(d_send) + slot * rp->chunk() * rp->elem_bytes;
+  return plan_run_fs(rp->rows, d_x, nullptr, dst, 1u << rp->log_r, false, io, S(s));
+}
+
+int ntt_rplan_forward_cols(ntt_rplan* rp, const void* d_recv, void* d_x, unsigned nvec, unsigned slot, void* s) {
+  if (!rp || !d_x || !d_recv || !nvec_ok(nvec, slot)) return NTT_ERR_ARG;
+  DeviceScope scope(rp->device);
+  FsIO io;
+  io.fs = FS_IL | (nvec > 1 ? FS_MAP_IN : 0u);
+  io.il = rp->log_c;
+  io.map_lc = rp->log_r + rp->log_c;
+  io.map_ps = nvec * rp->chunk();
+  const void* src = static_cast<const char*>(d_recv) + slot * rp->chunk() * rp->elem_bytes;
+  return plan_run_fs(rp->cols, src, nullptr, d_x, 1, false, io, S(s));
+}
+
+int ntt_rplan_inverse_cols(ntt_rplan* rp, const void* d_x, const void* d_y, void* d_send, void* s) {
+  if (!rp || !d_x || !d_send) return NTT_ERR_ARG;
+  DeviceScope scope(rp->device);
+  FsIO io;
+  io.fs = FS_IL;
+  io.il = rp->log_c;
+  io.tw_epi = rp->tab_inv;
+  return plan_run_fs(rp->cols, d_x, d_y, d_send, 1, true, io, S(s));
+}
+
+int ntt_rplan_inverse_rows(ntt_rplan* rp, const void* d_recv, void* d_out, void* s) {
+  if (!rp || !d_recv || !d_out) return NTT_ERR_ARG;
+  DeviceScope scope(rp->device);
+  FsIO io;
+  io.fs = FS_MAP_IN;
+  io.map_lc = rp->log_c;
+  io.map_ps = rp->chunk();
+  return plan_run_fs(rp->rows, d_recv, nullptr, d_out, 1u << rp->log_r, true, io, S(s));
+}
+
+int ntt_rplan_fill(ntt_rplan* rp, void* d_x, int kind, uint64_t seed, void* s) {
+  if (!rp || !d_x) return NTT_ERR_ARG;
+  // local element i = (a, j2) of the row layout: global j = g r + a + n1 j2
+  return ntt_fill_map(rp->tw, d_x, 1ull << (rp->log_n - rp->log_g), kind, seed, (uint64_t)rp->rank << rp->log_r,
+                      rp->log_n2, rp->log_n1, s);
+}
+
+int ntt_rplan_set_profiling(ntt_rplan* rp, int enable) {
+  if (!rp) return NTT_ERR_ARG;
+  int rc = ntt_plan_set_profiling(rp->rows, enable);
+  return rc ? rc : ntt_plan_set_profiling(rp->cols, enable);
+}
+
+int ntt_rplan_last_launch_ms(ntt_rplan* rp, int which, float* ms, unsigned max_launches, unsigned* nlaunches) {
+  if (!rp || (which != 0 && which != 1)) return NTT_ERR_ARG;
+  return ntt_plan_last_launch_ms(which ? rp->cols : rp->rows, ms, max_launches, nlaunches);
+}
+
+int ntt_rplan_destroy(ntt_rplan* rp) {
+  delete rp;
+  return NTT_OK;
+}
+
+}  // extern "C"

@@ -6,27 +6,28 @@ n = n1 * n2, j = j1 + n1*j2, k = k2 + n2*k1:
 
 Rank g of G (one process per GPU, ``torch.distributed`` over RCCL) owns
 
-* input, "row layout":    rows j1 in [g r, (g+1) r), r = n1/G; local [r][n2], element (a, j2) = x[g r + a + n1 j2]
-* output, "column layout": cols k2 in [g c, (g+1) c), c = n2/G; local [c][n1], element (kc, k1) = X[g c + kc + n2 k1]
+* input, "row layout":     rows j1 in [g r, (g+1) r), r = n1/G; local [r][n2], element (a, j2) = x[g r + a + n1 j2]
+* output, "column layout": cols k2 in [g c, (g+1) c), c = n2/G; local [n1][c], element (k1, kc) = X[g c + kc + n2 k1]
 
-Forward = batched n2-point NTTs of the local rows (libntt) -> twiddle w_n^(j1 k2) fused with the pack
-into per-peer chunks (libntt ntt_twiddle_pack) -> ONE all-to-all (RCCL; each peer chunk r*c elements)
--> local transpose (libntt) -> batched n1-point NTTs (libntt).  The inverse mirrors it (column layout
-in, row layout out), so forward/inverse/pointwise products (polynomial multiply) never leave the
-distributed layouts.  Gathering to natural order is a separate, test-only helper.
+Forward (libntt ``ntt_rplan_*``, ntt_amd/csrc/ntt_rplan.cpp) = batched n2-point NTTs of the local rows
+whose last pass multiplies by w_n^(j1 k2) and stores straight into per-peer chunks -> ONE all-to-all
+(RCCL; each peer chunk r*c elements) -> c interleaved n1-point NTTs that read the chunks where they
+arrived.  No separate twiddle, pack or transpose pass.  The inverse mirrors it (column layout in, row
+layout out), so forward / inverse / pointwise products never leave the distributed layouts.
 
-Polynomial multiply (BASELINE config 5): forward(a) and forward(b) pack into one send
-buffer [G][2][r*c] so that ONE all-to-all carries both; the pointwise product is local and fused
-into the first column pass of the inverse (ntt_inverse_pointwise_batch); the inverse's all-to-all
-returns c = a*b to the row layout.  Three transforms, two exchanges.
+Polynomial multiply (BASELINE config 5): forward(a) and forward(b) pack into one send buffer
+[G][2][r*c] so that ONE all-to-all carries both; the pointwise product is local and fused into the
+first column pass of the inverse; the inverse's all-to-all returns c = a*b to the row layout.  Three
+transforms, two exchanges.
 
 The reference has no multi-GPU code at all (no NCCL/MPI); this is new.
 The orchestration (FourStep) is engine- and transport-agnostic so the same code runs with the
-HIP engine over RCCL on GPUs, with G "virtual ranks" in one process on one GPU (exchange =
+HIP rank plan over RCCL on GPUs, with G "virtual ranks" in one process on one GPU (exchange =
 device copies), and with a CPU test engine over gloo.
 """
 from __future__ import annotations
 
+import ctypes as C
 from dataclasses import dataclass
 from typing import Callable, List, Optional
 
@@ -53,6 +54,7 @@ class Layout:
         self.n1, self.n2 = 1 << self.log_n1, 1 << self.log_n2
         self.r, self.c = 1 << self.log_r, 1 << self.log_c
         self.local_n = self.n >> self.log_g
+        self.chunk = self.r * self.c  # elements per peer chunk of one vector
 
     # global index of local element i (tests / fills)
     def row_global(self, i: int) -> int:
@@ -60,19 +62,18 @@ class Layout:
         return self.rank * self.r + a + self.n1 * j2
 
     def col_global(self, i: int) -> int:
-        kc, k1 = i >> self.log_n1, i & (self.n1 - 1)
+        k1, kc = i >> self.log_c, i & (self.c - 1)
         return self.rank * self.c + kc + self.n2 * k1
 
 
 class FourStep:
     """Per-rank four-step schedule over an engine (local compute) and an exchange (all-to-all).
 
-    Engine interface: ``rows_forward/rows_inverse(t, batch)`` (batched n2-point NTTs),
-    ``cols_forward/cols_inverse(t, batch)`` (batched n1-point NTTs), ``cols_inverse_pointwise(a, b,
-    out, batch)`` (out = batched n1-point INTT of a*b), ``twiddle_pack(src, dst, log_rows, log_len,
-    log_block, row0, inverse, peer_stride)``, ``transpose(src, dst, log_rows, log_cols,
-    log_block_rows, block_stride)``, ``empty(count)``.  Exchange: ``exchange(send, recv)`` =
-    all-to-all of equal contiguous chunks.
+    Engine interface (one rank): ``forward_rows(x, send, nvec, slot)`` (row layout -> peer chunks),
+    ``forward_cols(recv, x, nvec, slot)`` (received chunks -> column layout), ``inverse_cols(x, y,
+    send)`` (column layout, times y if given -> peer chunks), ``inverse_rows(recv, out)`` (-> row
+    layout), ``empty(count)``.  Buffers hold [G][nvec][chunk] elements.  Exchange:
+    ``exchange(send, recv)`` = all-to-all of equal contiguous chunks.
     """
 
     def __init__(self, layout: Layout, engine, exchange: Optional[Callable] = None):
@@ -83,132 +84,129 @@ class FourStep:
         self.recv = engine.empty(layout.local_n)
         self.send2 = self.recv2 = None  # [G][2][chunk]: the polymul's batched exchange, on first use
 
-    @property
-    def chunk(self) -> int:
-        return self.L.r * self.L.c
-
-    # ---- forward: row layout -> column layout (in place on x)
-    def forward_phase1(self, x, send=None, slot: int = 0, nslots: int = 1):
-        L = self.L
-        send = self.send if send is None else send
-        self.eng.rows_forward(x, L.r)
-        self.eng.twiddle_pack(x, send[slot * self.chunk:], L.log_r, L.log_n2, L.log_c, L.rank * L.r, False,
-                              nslots * self.chunk)
-
-    def forward_phase2(self, x, recv=None, slot: int = 0, nslots: int = 1):
-        L = self.L
-        recv = self.recv if recv is None else recv
-        # recv = [G][nslots][r][c]: row block g (rows g r ..) of this vector at (g nslots + slot) chunk
-        self.eng.transpose(recv[slot * self.chunk:], x, L.log_n1, L.log_c, L.log_r, nslots * self.chunk)
-        self.eng.cols_forward(x, L.c)
-
-    def forward(self, x):
-        self.forward_phase1(x)
-        self.exchange(self.send, self.recv)
-        self.forward_phase2(x)
-        return x
-
-    # ---- inverse: column layout -> row layout (in place on x)
-    def inverse_phase1(self, x, b=None, out=None):
-        """With b: out = INTT(x * b) (the polymul's fused pointwise product); else in place on x."""
-        L = self.L
-        if b is None:
-            self.eng.cols_inverse(x, L.c)
-            out = x
-        else:
-            self.eng.cols_inverse_pointwise(x, b, out, L.c)
-        self.eng.twiddle_pack(out, self.send, L.log_c, L.log_n1, L.log_r, L.rank * L.c, True, self.chunk)
-
-    def inverse_phase2(self, x):
-        L = self.L
-        self.eng.transpose(self.recv, x, L.log_n2, L.log_r, L.log_n2, L.local_n)  # recv = [G][c][r] = [n2][r]
-        self.eng.rows_inverse(x, L.r)
-
-    def inverse(self, x):
-        self.inverse_phase1(x)
-        self.exchange(self.send, self.recv)
-        self.inverse_phase2(x)
-        return x
-
-    # ---- polynomial multiply: row-layout a, b -> row-layout out = a * b (cyclic, length n).
-    # a and b are left holding their column-layout forward transforms (unless out aliases them).
     def pair_buffers(self):
         if self.send2 is None:
             self.send2 = self.eng.empty(2 * self.L.local_n)
             self.recv2 = self.eng.empty(2 * self.L.local_n)
         return self.send2, self.recv2
 
+    # ---- forward: row layout -> column layout (in place on x)
+    def forward_phase1(self, x):
+        self.eng.forward_rows(x, self.send, 1, 0)
+        return self.send, self.recv
+
+    def forward_phase2(self, x):
+        self.eng.forward_cols(self.recv, x, 1, 0)
+
+    def forward(self, x):
+        self.exchange(*self.forward_phase1(x))
+        self.forward_phase2(x)
+        return x
+
+    # ---- inverse: column layout -> row layout (in place on x, or into out with a pointwise factor y)
+    def inverse_phase1(self, x, y=None):
+        self.eng.inverse_cols(x, y, self.send)
+        return self.send, self.recv
+
+    def inverse_phase2(self, out):
+        self.eng.inverse_rows(self.recv, out)
+
+    def inverse(self, x):
+        self.exchange(*self.inverse_phase1(x))
+        self.inverse_phase2(x)
+        return x
+
+    # ---- polynomial multiply: row-layout a, b -> row-layout out = a * b (cyclic, length n).
+    # a and b are left holding their column-layout forward transforms (unless out aliases them).
     def polymul_phase1(self, a, b):
-        if a is b:
-            self.forward_phase1(a)
-            return self.send, self.recv
+        if a is b:  # squaring: one forward, single-vector exchange
+            return self.forward_phase1(a)
         send2, recv2 = self.pair_buffers()
-        self.forward_phase1(a, send2, 0, 2)
-        self.forward_phase1(b, send2, 1, 2)
+        self.eng.forward_rows(a, send2, 2, 0)
+        self.eng.forward_rows(b, send2, 2, 1)
         return send2, recv2
 
-    def polymul_phase2(self, a, b, out):
+    def polymul_phase2(self, a, b):
         if a is b:
             self.forward_phase2(a)
         else:
-            self.forward_phase2(a, self.recv2, 0, 2)
-            self.forward_phase2(b, self.recv2, 1, 2)
-        self.inverse_phase1(a, b, out)
+            self.eng.forward_cols(self.recv2, a, 2, 0)
+            self.eng.forward_cols(self.recv2, b, 2, 1)
+        return self.inverse_phase1(a, b)
 
     def polymul(self, a, b, out):
-        send, recv = self.polymul_phase1(a, b)
-        self.exchange(send, recv)
-        self.polymul_phase2(a, b, out)
-        self.exchange(self.send, self.recv)
+        self.exchange(*self.polymul_phase1(a, b))
+        self.exchange(*self.polymul_phase2(a, b))
         self.inverse_phase2(out)
         return out
 
 
-class HipEngine:
-    """Local steps on one GPU through libntt (the product path)."""
+class RankPlan:
+    """libntt ``ntt_rplan``: one rank's fused local steps on one GPU (the product path)."""
 
-    def __init__(self, field_id: int, log_n: int, limbs64: int, world: int, device: int):
-        from .ntt import NTTPlan
-        L = Layout(log_n, world, 0)
-        # separate row and column plans even when n1 == n2: their per-launch timing rings then hold
-        # one kernel shape each (bench.py reports them apart)
-        self.rows = NTTPlan(field_id, L.log_n2, limbs64, device)
-        self.cols = NTTPlan(field_id, L.log_n1, limbs64, device)
-        self.tw = NTTPlan(field_id, log_n, limbs64, device, twiddle_only=True)
+    def __init__(self, field_id: int, log_n: int, limbs64: int, world: int, rank: int, device: int):
+        from . import lib as _L
+        self._L = _L
+        self.lib = _L.load()
         self.limbs64 = limbs64
         self.device = device
+        h = C.c_void_p()
+        _L.check(self.lib.ntt_rplan_create(C.byref(h), field_id, log_n, limbs64, world, rank, device),
+                 "ntt_rplan_create")
+        self.handle = h
+        self.layout = Layout(log_n, world, rank)
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            self.lib.ntt_rplan_destroy(h)
+            self.handle = None
 
     def empty(self, count: int) -> torch.Tensor:
         shape = (count,) if self.limbs64 == 1 else (count, self.limbs64)
         return torch.empty(shape, dtype=torch.int64, device=f"cuda:{self.device}")
 
-    def rows_forward(self, t, batch):
-        self.rows.forward_batch(t, batch)
+    @staticmethod
+    def _p(t):
+        return C.c_void_p(t.data_ptr()) if t is not None else None
 
-    def rows_inverse(self, t, batch):
-        self.rows.inverse_batch(t, batch)
+    def _s(self, t):
+        return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
-    def cols_forward(self, t, batch):
-        self.cols.forward_batch(t, batch)
+    def forward_rows(self, x, send, nvec, slot):
+        self._L.check(self.lib.ntt_rplan_forward_rows(self.handle, self._p(x), self._p(send), nvec, slot, self._s(x)),
+                      "ntt_rplan_forward_rows")
 
-    def cols_inverse(self, t, batch):
-        self.cols.inverse_batch(t, batch)
+    def forward_cols(self, recv, x, nvec, slot):
+        self._L.check(self.lib.ntt_rplan_forward_cols(self.handle, self._p(recv), self._p(x), nvec, slot, self._s(x)),
+                      "ntt_rplan_forward_cols")
 
-    def cols_inverse_pointwise(self, a, b, out, batch):
-        self.cols.inverse_pointwise_batch(a, b, out, batch)
+    def inverse_cols(self, x, y, send):
+        self._L.check(self.lib.ntt_rplan_inverse_cols(self.handle, self._p(x), self._p(y), self._p(send), self._s(x)),
+                      "ntt_rplan_inverse_cols")
 
-    def twiddle_pack(self, src, dst, log_rows, log_len, log_block, row0, inverse, peer_stride=None):
-        self.tw.twiddle_pack(src, dst, log_rows, log_len, log_block, row0, inverse, peer_stride=peer_stride)
+    def inverse_rows(self, recv, out):
+        self._L.check(self.lib.ntt_rplan_inverse_rows(self.handle, self._p(recv), self._p(out), self._s(out)),
+                      "ntt_rplan_inverse_rows")
 
-    def transpose(self, src, dst, log_rows, log_cols, log_block_rows=None, block_stride=None):
-        self.tw.transpose(src, dst, log_rows, log_cols, log_block_rows=log_block_rows, block_stride=block_stride)
+    def fill(self, t, kind: str = "random", seed: int = 1):
+        k = {"iota": 0, "random": 1}[kind]
+        self._L.check(self.lib.ntt_rplan_fill(self.handle, self._p(t), k, int(seed), self._s(t)), "ntt_rplan_fill")
+        return t
 
-    def plans(self):
-        return [self.rows, self.cols]
+    def set_profiling(self, enable: bool = True) -> None:
+        self._L.check(self.lib.ntt_rplan_set_profiling(self.handle, int(bool(enable))), "ntt_rplan_set_profiling")
+
+    def last_launch_ms(self, which: int) -> List[float]:
+        buf = (C.c_float * 16)()
+        k = C.c_uint()
+        self._L.check(self.lib.ntt_rplan_last_launch_ms(self.handle, which, buf, 16, C.byref(k)),
+                      "ntt_rplan_last_launch_ms")
+        return [buf[i] for i in range(k.value)]
 
 
 class DistNTT:
-    """One rank of a distributed NTT: HIP engine + torch.distributed all-to-all (RCCL on GPUs).
+    """One rank of a distributed NTT: the fused rank plan + torch.distributed all-to-all (RCCL on GPUs).
 
     The default process group must be initialised (``nccl`` backend = RCCL on ROCm).  ``forward``
     takes this rank's row-layout share and leaves its column-layout share in place; ``inverse`` the
@@ -227,10 +225,10 @@ class DistNTT:
         self.device = device
         self.field_id, self.log_n, self.limbs64 = field_id, log_n, limbs64
         self.layout = Layout(log_n, world, rank)
-        self.engine = HipEngine(field_id, log_n, limbs64, world, device)
+        self.engine = RankPlan(field_id, log_n, limbs64, world, rank, device)
         self.fs = FourStep(self.layout, self.engine, self._exchange)
         self.n = self.layout.n
-        self.passes = self.engine.rows.passes
+        self.passes: List[int] = []  # per-transform schedules: see the row / column plans
 
     # RCCL moves < 2 GiB per peer per collective (a 2 GiB chunk arrived half copied,
     # tests/test_gpu_fullsize.py): larger per-peer chunks go as several all-to-alls of pieces.
@@ -255,9 +253,7 @@ class DistNTT:
 
     def fill(self, t: torch.Tensor, kind: str = "random", seed: int = 1) -> torch.Tensor:
         """This rank's row-layout share of the global synthetic vector (same values as NTTPlan.fill)."""
-        L = self.layout
-        self.engine.tw.fill_map(t, kind, seed, L.rank * L.r, L.log_n2, L.log_n1)
-        return t
+        return self.engine.fill(t, kind, seed)
 
     def forward(self, t: torch.Tensor) -> torch.Tensor:
         return self.fs.forward(t)
@@ -270,14 +266,11 @@ class DistNTT:
         return self.fs.polymul(a, b, out)
 
     def set_profiling(self, enable: bool = True) -> None:
-        for p in self.engine.plans():
-            p.set_profiling(enable)
+        self.engine.set_profiling(enable)
 
     def last_launch_ms(self) -> List[float]:
-        out: List[float] = []
-        for p in self.engine.plans():
-            out += p.last_launch_ms()
-        return out
+        """Row-transform launches, then column-transform launches (separate timing rings)."""
+        return self.engine.last_launch_ms(0) + self.engine.last_launch_ms(1)
 
 
 class VirtualRanks:
@@ -288,50 +281,41 @@ class VirtualRanks:
 
     def __init__(self, field_id: int, log_n: int, limbs64: int, world: int, device: int = 0):
         self.world = world
-        self.engine = HipEngine(field_id, log_n, limbs64, world, device)
-        self.ranks = [FourStep(Layout(log_n, world, g), self.engine) for g in range(world)]
+        self.engines = [RankPlan(field_id, log_n, limbs64, world, g, device) for g in range(world)]
+        self.ranks = [FourStep(Layout(log_n, world, g), e) for g, e in enumerate(self.engines)]
         self.layout0 = self.ranks[0].L
 
-    def _exchange_all(self, sends=None, recvs=None):
+    def _exchange_all(self, bufs):
         G = self.world
-        sends = sends or [fs.send for fs in self.ranks]
-        recvs = recvs or [fs.recv for fs in self.ranks]
+        sends, recvs = [s for s, _ in bufs], [r for _, r in bufs]
         chunk = sends[0].shape[0] // G
         for dst in range(G):
             for src in range(G):
                 recvs[dst][src * chunk:(src + 1) * chunk].copy_(sends[src][dst * chunk:(dst + 1) * chunk])
 
     def empty(self) -> List[torch.Tensor]:
-        return [self.engine.empty(self.layout0.local_n) for _ in range(self.world)]
+        return [e.empty(self.layout0.local_n) for e in self.engines]
 
     def fill(self, xs: List[torch.Tensor], kind: str = "random", seed: int = 1):
-        for g, t in enumerate(xs):
-            L = self.ranks[g].L
-            self.engine.tw.fill_map(t, kind, seed, g * L.r, L.log_n2, L.log_n1)
+        for e, t in zip(self.engines, xs):
+            e.fill(t, kind, seed)
         return xs
 
     def forward(self, xs: List[torch.Tensor]):
-        for fs, x in zip(self.ranks, xs):
-            fs.forward_phase1(x)
-        self._exchange_all()
+        self._exchange_all([fs.forward_phase1(x) for fs, x in zip(self.ranks, xs)])
         for fs, x in zip(self.ranks, xs):
             fs.forward_phase2(x)
         return xs
 
     def inverse(self, xs: List[torch.Tensor]):
-        for fs, x in zip(self.ranks, xs):
-            fs.inverse_phase1(x)
-        self._exchange_all()
+        self._exchange_all([fs.inverse_phase1(x) for fs, x in zip(self.ranks, xs)])
         for fs, x in zip(self.ranks, xs):
             fs.inverse_phase2(x)
         return xs
 
     def polymul(self, As: List[torch.Tensor], Bs: List[torch.Tensor], Outs: List[torch.Tensor]):
-        bufs = [fs.polymul_phase1(a, b) for fs, a, b in zip(self.ranks, As, Bs)]
-        self._exchange_all([s for s, _ in bufs], [r for _, r in bufs])
-        for fs, a, b, o in zip(self.ranks, As, Bs, Outs):
-            fs.polymul_phase2(a, b, o)
-        self._exchange_all()
+        self._exchange_all([fs.polymul_phase1(a, b) for fs, a, b in zip(self.ranks, As, Bs)])
+        self._exchange_all([fs.polymul_phase2(a, b) for fs, a, b in zip(self.ranks, As, Bs)])
         for fs, o in zip(self.ranks, Outs):
             fs.inverse_phase2(o)
         return Outs
@@ -344,9 +328,8 @@ class MultiPlan:
     """
 
     def __init__(self, field_id: int = 1, log_n: int = 24, limbs64: int = 4, devices: Optional[List[int]] = None):
-        import ctypes as C
         from . import lib as _L
-        self._C, self._L = C, _L
+        self._L = _L
         self.lib = _L.load()
         self.devices = list(devices if devices is not None else range(torch.cuda.device_count()))
         self.limbs64 = limbs64
@@ -371,7 +354,6 @@ class MultiPlan:
         return [torch.empty(shape, dtype=torch.int64, device=f"cuda:{d}") for d in self.devices]
 
     def _ptrs(self, xs):
-        C = self._C
         for t, d in zip(xs, self.devices):
             if not t.is_contiguous() or t.device.index != d or t.numel() * 8 != self.local_n * 8 * self.limbs64:
                 raise ValueError("each share must be a contiguous tensor of local_n elements on its device")

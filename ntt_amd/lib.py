@@ -64,6 +64,17 @@ PROTOTYPES = {
                                       _vp]),
     "ntt_transpose_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint, C.c_uint, C.c_uint, C.c_uint64, _vp]),
     "ntt_polymul_multi": (C.c_int, [_vp, C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp), C.POINTER(_vp)]),
+    "ntt_rplan_create": (C.c_int, [C.POINTER(_vp), C.c_int, C.c_uint, C.c_uint, C.c_int, C.c_int, C.c_int]),
+    "ntt_rplan_info": (C.c_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint),
+                                 C.POINTER(C.c_uint), C.POINTER(C.c_uint)]),
+    "ntt_rplan_forward_rows": (C.c_int, [_vp, _vp, _vp, C.c_uint, C.c_uint, _vp]),
+    "ntt_rplan_forward_cols": (C.c_int, [_vp, _vp, _vp, C.c_uint, C.c_uint, _vp]),
+    "ntt_rplan_inverse_cols": (C.c_int, [_vp, _vp, _vp, _vp, _vp]),
+    "ntt_rplan_inverse_rows": (C.c_int, [_vp, _vp, _vp, _vp]),
+    "ntt_rplan_fill": (C.c_int, [_vp, _vp, C.c_int, C.c_uint64, _vp]),
+    "ntt_rplan_set_profiling": (C.c_int, [_vp, C.c_int]),
+    "ntt_rplan_last_launch_ms": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_float), C.c_uint, C.POINTER(C.c_uint)]),
+    "ntt_rplan_destroy": (C.c_int, [_vp]),
 }
 
 _lock = threading.Lock()

@@ -1,5 +1,11 @@
 """Test doubles for the distributed four-step: a CPU engine backed by the C oracle (the checker),
-used to run ntt_amd.distributed.FourStep over gloo on CPU.  Not product code."""
+used to run ntt_amd.distributed.FourStep over gloo on CPU.  Not product code.
+
+It implements the rank-plan interface (ntt_rplan_*, ntt_amd/csrc/ntt_rplan.cpp) with the same
+layouts: row layout [r][n2], column layout [n1][c], send / receive buffers [G][nvec][r c] where the
+forward's chunk for peer q holds [a][kc] (rows a of this rank, columns q c + kc) and the inverse's
+chunk for peer q holds [j1 - q r][kc] (this rank's columns).
+"""
 import numpy as np
 import torch
 
@@ -8,63 +14,73 @@ from oracle import oracle_c as OC
 
 
 class CpuOracleEngine:
-    def __init__(self, field_id, log_n, limbs64):
+    def __init__(self, field_id, log_n, limbs64, world=1, rank=0):
         from ntt_amd.distributed import Layout
         self.p, self.g = R.FIELDS[field_id]
         self.L = limbs64
-        self.log_n = log_n
-        lay = Layout(log_n, 1, 0)
-        self.n1, self.n2 = lay.n1, lay.n2
+        self.lay = Layout(log_n, world, rank)
         n = 1 << log_n
         w = R.root_of_unity(self.p, self.g, n)
-        self.pw = [pow(w, e, self.p) for e in range(n)]
-        winv = pow(w, self.p - 2, self.p)
-        self.pw_inv = [pow(winv, e, self.p) for e in range(n)]
+        self.w, self.winv, self.n = w, pow(w, self.p - 2, self.p), n
 
     def empty(self, count):
         return torch.zeros((count, self.L), dtype=torch.int64)
 
-    def _rows(self, t, batch, inverse):
-        a = t.numpy().view(np.uint64).reshape(batch, -1, self.L)
-        for i in range(batch):
-            a[i] = OC.ntt_mp(a[i], self.p, self.g, inverse)
+    def _ints(self, t):
+        return OC.limbs_to_ints(t.numpy().view(np.uint64).reshape(-1, self.L))
 
-    def rows_forward(self, t, batch):
-        self._rows(t, batch, False)
+    def _put(self, t, idx, vals):
+        a = t.numpy().view(np.uint64).reshape(-1, self.L)
+        a[np.asarray(idx)] = OC.ints_to_limbs(vals, self.L)
 
-    def rows_inverse(self, t, batch):
-        self._rows(t, batch, True)
+    def _ntt(self, vals, inverse):
+        return OC.limbs_to_ints(OC.ntt_mp(OC.ints_to_limbs(vals, self.L), self.p, self.g, inverse))
 
-    cols_forward = rows_forward
-    cols_inverse = rows_inverse
+    def forward_rows(self, x, send, nvec, slot):
+        L, p = self.lay, self.p
+        xs = self._ints(x)
+        idx, vals = [], []
+        for a in range(L.r):
+            X = self._ntt(xs[a * L.n2:(a + 1) * L.n2], False)
+            j1 = L.rank * L.r + a
+            for k2 in range(L.n2):
+                q, kc = divmod(k2, L.c)
+                idx.append((q * nvec + slot) * L.chunk + a * L.c + kc)
+                vals.append(X[k2] * pow(self.w, j1 * k2 % self.n, p) % p)
+        self._put(send, idx, vals)
 
-    def cols_inverse_pointwise(self, a, b, out, batch):
-        n = a.shape[0] // batch
-        prod = OC.mul_mp(a.numpy().view(np.uint64).reshape(-1, self.L), b.numpy().view(np.uint64).reshape(-1, self.L),
-                         self.p)
-        for i in range(batch):
-            prod[i * n:(i + 1) * n] = OC.ntt_mp(prod[i * n:(i + 1) * n], self.p, self.g, True)
-        out.numpy().view(np.uint64).reshape(-1, self.L)[:] = prod
+    def forward_cols(self, recv, x, nvec, slot):
+        L = self.lay
+        rv = self._ints(recv)
+        out = [0] * L.local_n
+        for kc in range(L.c):
+            col = [rv[((j1 // L.r) * nvec + slot) * L.chunk + (j1 % L.r) * L.c + kc] for j1 in range(L.n1)]
+            for k1, v in enumerate(self._ntt(col, False)):
+                out[k1 * L.c + kc] = v
+        self._put(x, range(L.local_n), out)
 
-    def twiddle_pack(self, src, dst, log_rows, log_len, log_block, row0, inverse, peer_stride=None):
-        n = 1 << self.log_n
-        table = self.pw_inv if inverse else self.pw
-        s = OC.limbs_to_ints(src.numpy().view(np.uint64).reshape(-1, self.L))
-        rows, length, bw = 1 << log_rows, 1 << log_len, 1 << log_block
-        ps = rows * bw if peer_stride is None else peer_stride
-        d = dst.numpy().view(np.uint64).reshape(-1, self.L)
-        for a in range(rows):
-            for b in range(length):
-                v = s[a * length + b] * table[((row0 + a) * b) % n] % self.p
-                d[(b // bw) * ps + a * bw + (b % bw)] = OC.ints_to_limbs([v], self.L)[0]
+    def inverse_cols(self, x, y, send):
+        L, p = self.lay, self.p
+        xs = self._ints(x)
+        if y is not None:
+            ys = self._ints(y)
+            xs = [u * v % p for u, v in zip(xs, ys)]
+        out = [0] * L.local_n
+        for kc in range(L.c):
+            k2 = L.rank * L.c + kc
+            col = self._ntt([xs[k1 * L.c + kc] for k1 in range(L.n1)], True)
+            for j1, v in enumerate(col):
+                out[j1 * L.c + kc] = v * pow(self.winv, j1 * k2 % self.n, p) % p
+        self._put(send, range(L.local_n), out)
 
-    def transpose(self, src, dst, log_rows, log_cols, log_block_rows=None, block_stride=None):
-        lb = log_rows if log_block_rows is None else log_block_rows
-        bs = (1 << (lb + log_cols)) if block_stride is None else block_stride
-        s = src.numpy().view(np.uint64).reshape(-1, self.L)
-        rows, cols = 1 << log_rows, 1 << log_cols
-        m = np.stack([s[(r >> lb) * bs + (r & ((1 << lb) - 1)) * cols:][:cols] for r in range(rows)])
-        dst.numpy().view(np.uint64).reshape(-1, self.L)[:] = np.ascontiguousarray(m.transpose(1, 0, 2)).reshape(-1, self.L)
+    def inverse_rows(self, recv, out):
+        L = self.lay
+        rv = self._ints(recv)
+        res = [0] * L.local_n
+        for a in range(L.r):
+            row = [rv[(k2 // L.c) * L.chunk + a * L.c + (k2 % L.c)] for k2 in range(L.n2)]
+            res[a * L.n2:(a + 1) * L.n2] = self._ntt(row, True)
+        self._put(out, range(L.local_n), res)
 
 
 def row_shares(x_ints, layout_cls, log_n, world, L):

@@ -33,7 +33,7 @@ def _worker(rank, world, port, field_id, log_n, L, q):
         n = 1 << log_n
         x = R.random_vector(field_id, n, seed=77)
         share = row_shares(x, Layout, log_n, world, L)[rank]
-        eng = CpuOracleEngine(field_id, log_n, L)
+        eng = CpuOracleEngine(field_id, log_n, L, world, rank)
         fs = FourStep(Layout(log_n, world, rank), eng, lambda s, r: dist.all_to_all_single(r.view(-1), s.view(-1)))
         fs.forward(share)
         fwd = share.clone()
@@ -107,7 +107,7 @@ def _polymul_worker(rank, world, port, field_id, log_n, L, square, q):
         sa = row_shares(a, Layout, log_n, world, L)[rank]
         sb = sa if square else row_shares(b, Layout, log_n, world, L)[rank]
         out = torch.zeros_like(sa)
-        eng = CpuOracleEngine(field_id, log_n, L)
+        eng = CpuOracleEngine(field_id, log_n, L, world, rank)
         fs = FourStep(Layout(log_n, world, rank), eng, lambda s, r: dist.all_to_all_single(r.view(-1), s.view(-1)))
         fs.polymul(sa, sb, out)
         q.put((rank, out.numpy().tobytes()))

@@ -19,7 +19,7 @@ def _index(layout, kind):
     if kind == "row":
         a, j2 = i >> layout.log_n2, i & (layout.n2 - 1)
         return layout.rank * layout.r + a + layout.n1 * j2
-    kc, k1 = i >> layout.log_n1, i & (layout.n1 - 1)
+    k1, kc = i >> layout.log_c, i & (layout.c - 1)  # column layout [n1][c]
     return layout.rank * layout.c + kc + layout.n2 * k1
 
 
@@ -90,3 +90,47 @@ def test_mplan_single_process_rccl(log_n, field_id, L):
     mp.inverse(xs)
     for s, t in zip(shares, xs):
         assert torch.equal(s, t)
+
+
+@pytest.mark.parametrize("fid,L", [(1, 4), (0, 1), (2, 6)])
+def test_twiddle_pack_and_transpose_building_blocks(fid, L):
+    """ntt_twiddle_pack_ex / ntt_transpose_ex (C-ABI building blocks; the rank plan fuses them into
+    the transform passes): against the closed forms on the host."""
+    from ntt_amd.ntt import NTTPlan
+    from oracle import ntt_ref as R
+    from oracle import oracle_c as OC
+    import numpy as np
+    p, g = R.FIELDS[fid]
+    log_n, lr, ll, lb = 12, 3, 6, 4
+    pl = NTTPlan(fid, log_n, L, twiddle_only=True)
+    n = 1 << log_n
+    w = R.root_of_unity(p, g, n)
+    rows, length, bw = 1 << lr, 1 << ll, 1 << lb
+    src_np = OC.random_limbs(fid, rows * length, seed=3, L=L)
+    src = torch.from_numpy(src_np.view(np.int64)).to("cuda:0").reshape(-1, L) if L > 1 else \
+        torch.from_numpy(src_np.view(np.int64).reshape(-1)).to("cuda:0")
+    ps = 2 * rows * bw
+    dst = torch.zeros((length // bw) * ps * L, dtype=torch.int64, device="cuda:0")
+    dst = dst.reshape(-1, L) if L > 1 else dst
+    row0 = 5
+    pl.twiddle_pack(src, dst, lr, ll, lb, row0, False, peer_stride=ps)
+    got = OC.limbs_to_ints(dst.cpu().numpy().view(np.uint64).reshape(-1, L))
+    sv = OC.limbs_to_ints(src_np)
+    for a in range(rows):
+        for b in range(length):
+            assert got[(b // bw) * ps + a * bw + b % bw] == sv[a * length + b] * pow(w, (row0 + a) * b % n, p) % p
+    # transpose of a matrix whose row blocks are spread at block_stride
+    lrows, lcols, lbr = 5, 3, 2
+    bs = 3 * (1 << (lbr + lcols))
+    nblk = 1 << (lrows - lbr)
+    src2 = torch.arange(nblk * bs * L, dtype=torch.int64, device="cuda:0")
+    src2 = src2.reshape(-1, L) if L > 1 else src2
+    out = torch.empty(((1 << (lrows + lcols)), L) if L > 1 else (1 << (lrows + lcols),), dtype=torch.int64,
+                      device="cuda:0")
+    pl.transpose(src2, out, lrows, lcols, log_block_rows=lbr, block_stride=bs)
+    s2 = src2.cpu().reshape(nblk * bs, -1)
+    o = out.cpu().reshape(1 << lcols, 1 << lrows, -1)
+    for r_ in range(1 << lrows):
+        for c_ in range(1 << lcols):
+            srow = (r_ >> lbr) * bs + (r_ & ((1 << lbr) - 1)) * (1 << lcols) + c_
+            assert torch.equal(o[c_, r_], s2[srow])

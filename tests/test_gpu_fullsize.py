@@ -62,7 +62,7 @@ def _kat_check_columns(shares, layouts, n, p, g, L, ks):
     for k in ks:
         k2, k1 = k % layouts[0].n2, k // layouts[0].n2
         rank, kc = k2 // layouts[0].c, k2 % layouts[0].c
-        row = shares[rank][kc * layouts[0].n1 + k1].cpu().numpy().view(np.uint64).reshape(-1)
+        row = shares[rank][k1 * layouts[0].c + kc].cpu().numpy().view(np.uint64).reshape(-1)  # [n1][c]
         v = sum(int(row[i]) << (64 * i) for i in range(L))
         assert v == R.kat_xj(n, p, g, k), k
 
