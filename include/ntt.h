@@ -64,6 +64,14 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
  * pointwise product becomes the Montgomery product a b R^-1 so that polymul maps (a R, b R) to
  * (a b) R.  Saves the caller a to/from-Montgomery pass over the data on each side. */
 #define NTT_PLAN_MONTGOMERY_IO 2u
+/* Rival schedule: forward transforms run as the reference's bellperson / improved_NTT
+ * family re-derived for gfx950 — Stockham autosort passes of radix 2^r_i with the twiddle applied to
+ * the INPUT of each pass (GZKP-NTT.cu:324-386 FIELD_radix_fft; :556-1296 improved_NTT_v1..v4, whose
+ * grouping / coalescing / bank-conflict variants the wave64 LDS-staged kernels subsume), ping-pong
+ * between two plan buffers, no final digit-reversal pass.  Same contract and results as the default
+ * four-step DIF schedule; kept to measure against it (tools/bench_rivals.py).  P469762049 (1 limb)
+ * and 4-limb plans, single transforms (batch 1); other calls use the default schedule. */
+#define NTT_PLAN_STOCKHAM 4u
 int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags);
 
 /* Modulus-generic plan, like big-num.cu's `prime` / `omega` kernel arguments (big-num.cu:68,173,260):

@@ -1,0 +1,5 @@
+// EngP: k_pass instantiations for KIND_STOCKHAM (the reference's bellperson-family rival schedule).
+#include "ntt_kernels_impl.hpp"
+namespace ntt {
+NTT_INSTANTIATE_KIND(EngP, KIND_STOCKHAM)
+}  // namespace ntt

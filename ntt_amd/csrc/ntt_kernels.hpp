@@ -6,7 +6,15 @@
 
 namespace ntt {
 
-enum : int { KIND_COLUMN = 0, KIND_FINAL = 1, KIND_SINGLE = 2 };
+// KIND_STOCKHAM: the rival schedule of the reference's bellperson / improved_NTT_v1..v4 family
+// (GZKP-NTT.cu:324-386, 556-1296): Stockham autosort passes, input-side twiddles, no final
+// permutation (ntt_plan_create_ex flag NTT_PLAN_STOCKHAM).
+enum : int { KIND_COLUMN = 0, KIND_FINAL = 1, KIND_SINGLE = 2, KIND_STOCKHAM = 3 };
+// engines with KIND_STOCKHAM instances (ntt_e256_stk.hip, ntt_ep_stk.hip)
+template <class E>
+struct HasStockham {
+  static constexpr bool value = false;
+};
 
 // Elements per workgroup tile of the multi-pass kernels (engines.hpp: E::TILE_LOG, E::EPT per thread).
 template <class E>
@@ -16,6 +24,14 @@ using Eng256 = Eng29<9, 8>;    // 4 x 64-bit limbs in HBM
 using Eng384 = Eng29<14, 12>;  // 6 x 64-bit limbs in HBM, moduli up to 2^383
 using Eng256w = Eng29<9, 12>;  // 6 x 64-bit limbs in HBM, moduli < 2^255 (256-bit arithmetic)
 using EngP = Eng32<1, 2>;      // P469762049, `long long` in HBM
+template <>
+struct HasStockham<Eng256> {
+  static constexpr bool value = true;
+};
+template <>
+struct HasStockham<EngP> {
+  static constexpr bool value = true;
+};
 
 // a modulus as W little-endian 32-bit words (canonical-range checks)
 template <int W>
@@ -53,6 +69,7 @@ struct PassArgs {
   // Mode I (fs & FS_IL): 2^il transforms interleaved, element j of transform b at j 2^il + b (the
   //   [n1][c] column layout); every pass groups T adjacent transforms, so runs stay contiguous.  A
   //   mapped input index P lives at (P >> map_lc) * map_ps + (P mod 2^map_lc) (peer chunks of r c).
+  uint32_t lgp;          // KIND_STOCKHAM: log2 of the number of groups p already combined (bellperson `lgp`)
   uint32_t fs;           // FS_* bits
   uint32_t il;           // Mode I: log2 of the interleave
   uint32_t map_lc;

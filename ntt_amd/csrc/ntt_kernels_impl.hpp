@@ -238,6 +238,7 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                               const PassArgs<E> A) {
   constexpr int QB = ept_log<E>(), EPT = E::EPT;
   using S = Sched<LOGR, QB>;
+  constexpr bool COLLIKE = KIND == KIND_COLUMN || KIND == KIND_STOCKHAM;  // column-group geometry
   constexpr int TE = (KIND == KIND_SINGLE) ? (1 << LOGR) : (1 << tile_log_of<E>());
   constexpr int T = TE >> LOGR;  // columns (column pass) or blocks (final / single) per workgroup
   constexpr int NT = TE / EPT;   // threads
@@ -247,6 +248,7 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
   // HBM words per element: the caller's buffers hold E::MEMW, the plan's scratch and outer-twiddle
   // tables E::SCRW (8 for 256-bit values in the 48-B layout).  Column passes read the caller's
   // buffer (pass 1, SRC_USER) or scratch and write scratch; the final pass reads scratch.
+  // (Stockham passes ping-pong between caller-format buffers: E::MEMW words both ways)
   constexpr int SW = (KIND == KIND_COLUMN) ? (SRC_USER ? E::MEMW : E::SCRW) : (KIND == KIND_FINAL ? E::SCRW : E::MEMW);
   constexpr int DW = (KIND == KIND_COLUMN) ? E::SCRW : E::MEMW;
 
@@ -291,7 +293,7 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
   uint32_t mid = 0, k10 = 0, midrev = 0;  // final pass
   uint32_t b0 = 0, tb_log = 0;            // final pass, Mode I: first transform, log2 transforms per WG
   const uint32_t w = blockIdx.x;
-  if constexpr (KIND == KIND_COLUMN) {
+  if constexpr (COLLIKE) {
     const uint32_t log_s = A.log_blk - LOGR;
     const uint32_t groups_log = log_s - __builtin_ctz(T);  // column groups per block (log)
     const size_t blk = w >> groups_log;
@@ -318,7 +320,7 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
       midrev |= d << A.mid_off[i];
     }
   }
-  const uint32_t log_s = (KIND == KIND_COLUMN) ? (A.log_blk - LOGR) : 0u;
+  const uint32_t log_s = COLLIKE ? (A.log_blk - LOGR) : 0u;
 
   uint32_t x[EPT][E::W];
   uint32_t cl[EPT / 2];   // local column/block of each group (<= EPT/2 groups per thread)
@@ -331,7 +333,7 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
       constexpr int j = J;
       const uint32_t lam = t + NT * j;
       uint32_t c, g;
-      if constexpr (KIND == KIND_COLUMN) {
+      if constexpr (COLLIKE) {
         c = lam % T;
         g = lam / T;
       } else {
@@ -344,7 +346,7 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
         constexpr int d = D;
         const uint32_t pi = g + (d << sb);
         size_t pos;
-        if constexpr (KIND == KIND_COLUMN) {
+        if constexpr (COLLIKE) {
           pos = colbase + c + ((size_t)pi << log_s);
         } else if constexpr (KIND == KIND_FINAL) {
           if (fs_il) {
@@ -359,6 +361,14 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
           pos = pi;
         }
         E::template load<SW>(x[j * Q + d], src, NTT_NOMEM(IN_USER ? in_pos(pos) : pos));
+        if constexpr (KIND == KIND_STOCKHAM && FULLTW) {
+          // bellperson's input twiddle (GZKP-NTT.cu:348-354): element pi of group k = index mod p is
+          // multiplied by w_n^((n >> lgp >> deg) k pi), from a [k / T][pi][k mod T] table (p >= T)
+          uint32_t tw[E::W];
+          const uint32_t k0 = col0 & ((1u << A.lgp) - 1);
+          E::template load<E::SCRW>(tw, A.tw_full, ((size_t)k0 << LOGR) + pi * T + c);
+          E::mulv(x[j * Q + d], tw, A.F);
+        }
         if constexpr (PRO == PRO_PW) {
           uint32_t y[E::W];
           E::load(y, A.src2 + boff, pos);
@@ -406,7 +416,12 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
         const uint32_t pi = (rho << lN) + cp + (k << sb);
         const uint32_t kn = natural_index<LOGR, QB>(pi);
         size_t pos;
-        if constexpr (KIND == KIND_COLUMN) {
+        if constexpr (KIND == KIND_STOCKHAM) {
+          // autosort store (GZKP-NTT.cu:378-384): y[((index - k) << deg) + k + kn p], k = index mod p
+          const uint32_t idx = col0 + c, kk = idx & ((1u << A.lgp) - 1);
+          pos = ((size_t)(idx - kk) << LOGR) + kk + ((size_t)kn << A.lgp);
+          E::template store<E::IN * Q, FAST, DW>(dst, NTT_NOMEM(pos), v, A.F);
+        } else if constexpr (KIND == KIND_COLUMN) {
           if constexpr (FULLTW) {
             // outer twiddle w_{N_i}^{col * kn} R_e from the per-pass table (HBM element format,
             // column-group-major [col / T][kn][col mod T], so one workgroup's entries are one
@@ -814,6 +829,10 @@ static hipError_t launch_plain(const uint32_t* src, uint32_t* dst, const PassArg
 template <class E, int KIND, int LOGR, bool FULLTW, bool FAST>
 static hipError_t launch_fsm(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, dim3 g, dim3 b,
                              hipStream_t st) {
+  if constexpr (KIND == KIND_STOCKHAM) {
+    if (A.fs || A.tw_epi) return hipErrorInvalidValue;
+    return launch_plain<E, LOGR, KIND, FULLTW, FAST, 0>(src, dst, A, g, b, st);
+  }
   if (A.fs == 0 && !A.tw_epi) return launch_plain<E, LOGR, KIND, FULLTW, FAST, 0>(src, dst, A, g, b, st);
   if constexpr (KIND != KIND_COLUMN) {
     if (A.tw_epi) return launch_plain<E, LOGR, KIND, FULLTW, FAST, 2>(src, dst, A, g, b, st);
@@ -826,7 +845,7 @@ static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassAr
                                 uint32_t batch, hipStream_t st) {
   constexpr int TL = tile_log_of<E>();
   constexpr int MAXR = (KIND == KIND_SINGLE) ? TL : TL - E::MIN_COLS_LOG;
-  if constexpr (LOGR > MAXR) {
+  if constexpr (LOGR > MAXR || (KIND == KIND_STOCKHAM && !HasStockham<E>::value)) {
     return hipErrorInvalidValue;
   } else {
     constexpr int TE = (KIND == KIND_SINGLE) ? (1 << LOGR) : (1 << TL);
@@ -834,6 +853,10 @@ static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassAr
     const dim3 g(grid, batch), b(NT < 64 ? 64 : NT);
     if constexpr (E::FASTRED) {
       if (A.F.red_ok) {
+        if constexpr (KIND == KIND_STOCKHAM) {
+          return A.tw_full ? launch_fsm<E, KIND, LOGR, true, true>(src, dst, A, g, b, st)
+                           : launch_fsm<E, KIND, LOGR, false, true>(src, dst, A, g, b, st);
+        }
         if constexpr (KIND == KIND_COLUMN) {
           if (A.tw_full && A.src2) {
             if (A.fs)  // Mode I polymul inverse (ntt_rplan)
@@ -854,7 +877,7 @@ static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassAr
       }
     }
     if (A.src2 || A.tw_in) return hipErrorInvalidValue;
-    if constexpr (KIND == KIND_COLUMN) {
+    if constexpr (KIND == KIND_COLUMN || KIND == KIND_STOCKHAM) {
       if (A.tw_full) return launch_fsm<E, KIND, LOGR, true, false>(src, dst, A, g, b, st);
     }
     return launch_fsm<E, KIND, LOGR, false, false>(src, dst, A, g, b, st);
@@ -885,6 +908,11 @@ hipError_t launch_pass(int kind, int logr, const uint32_t* src, uint32_t* dst, c
                        uint32_t batch, hipStream_t st) {
   if (kind == KIND_COLUMN) return launch_pass_kind<E, KIND_COLUMN>(logr, src, dst, A, grid, batch, st);
   if (kind == KIND_FINAL) return launch_pass_kind<E, KIND_FINAL>(logr, src, dst, A, grid, batch, st);
+  if (kind == KIND_STOCKHAM) {
+    if constexpr (HasStockham<E>::value)
+      return launch_pass_kind<E, KIND_STOCKHAM>(logr, src, dst, A, grid, batch, st);
+    return hipErrorInvalidValue;
+  }
   return launch_pass_kind<E, KIND_SINGLE>(logr, src, dst, A, grid, batch, st);
 }
 
@@ -927,6 +955,7 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
   NTT_EXTERN_KIND(E, KIND_COLUMN)                                                                                  \
   NTT_EXTERN_KIND(E, KIND_FINAL)                                                                                   \
   NTT_EXTERN_KIND(E, KIND_SINGLE)                                                                                  \
+  NTT_EXTERN_KIND(E, KIND_STOCKHAM)                                                                                \
   template hipError_t launch_pass<E>(int, int, const uint32_t*, uint32_t*, const PassArgs<E>&, uint32_t, uint32_t, \
                                      hipStream_t);                                                                 \
   template hipError_t launch_naive<E>(const uint32_t*, uint32_t*, const PassArgs<E>&, uint32_t, hipStream_t);       \

@@ -303,6 +303,10 @@ struct PlanImpl final : PlanBase {
   size_t off_rm = 0;                    // R_e R^-1 (Montgomery-form pointwise product)
   size_t off_hi_ipm = 0;                // inverse hi table scaled by n^-1 R_e (fused polymul, pass 1)
   uint32_t* d_full_pm = nullptr;        // inverse pass-1 outer twiddles x n^-1 R_e (fused polymul)
+  uint32_t* d_stk_tab = nullptr;        // NTT_PLAN_STOCKHAM: per-pass input-twiddle tables
+  size_t stk_off[8] = {};               // element offsets into d_stk_tab (pass >= 1)
+  unsigned stk_ord[8] = {};             // Stockham pass i runs radix r[stk_ord[i]] (widest first)
+  uint32_t* d_stk_buf[2] = {nullptr, nullptr};  // NTT_PLAN_STOCKHAM ping-pong buffers (E::MEMW words)
   unsigned lo_bits = 0;
   uint32_t nrand = 1, top_bits = 28;
 
@@ -314,6 +318,9 @@ struct PlanImpl final : PlanBase {
     if (d_scratch) hipFree(d_scratch);
     if (d_full) hipFree(d_full);
     if (d_full_pm) hipFree(d_full_pm);
+    if (d_stk_tab) hipFree(d_stk_tab);
+    for (auto* p : d_stk_buf)
+      if (p) hipFree(p);
     if (d_bad) hipFree(d_bad);
     if (d_coset) hipFree(d_coset);
     if (d_coset_full) hipFree(d_coset_full);
@@ -481,8 +488,69 @@ struct PlanImpl final : PlanBase {
       rc = NTT_ERR_HIP;
     if (rc == NTT_OK && npass >= 2 && !twiddle_only) rc = ensure_scratch(1);
     if (rc == NTT_OK && npass >= 2 && !twiddle_only) rc = build_full_tables();
+    if (rc == NTT_OK && (flags & NTT_PLAN_STOCKHAM)) rc = build_stockham();
     hipSetDevice(cur);
     return rc;
+  }
+
+  // NTT_PLAN_STOCKHAM (rival schedule, bellperson family): pass i (i >= 1) multiplies element pi of
+  // group k < p_i = 2^(r_0 + ... + r_{i-1}) by w_n^((k pi) << (log_n - lgp_i - r_i)) from a table in
+  // the column-group-major layout of the pass kernels (k_build_tw with c := k); two ping-pong buffers.
+  int build_stockham() {
+    if constexpr (!HasStockham<E>::value) {
+      return NTT_ERR_ARG;
+    } else {
+      if (npass < 2) return NTT_ERR_ARG;
+      // widest radix first: pass i >= 1 needs p_i = 2^(r_0 + ... + r_{i-1}) >= T_i = TILE / R_i
+      for (unsigned i = 0; i < npass; ++i) stk_ord[i] = i;
+      std::stable_sort(stk_ord, stk_ord + npass, [&](unsigned a, unsigned b) { return r[a] > r[b]; });
+      size_t elems = 0;
+      unsigned lgp = 0;
+      const unsigned tl = tile_log_of<E>();
+      for (unsigned i = 0; i < npass; ++i) {
+        const unsigned ri = r[stk_ord[i]];
+        if (i > 0) {
+          if (lgp + ri < tl) return NTT_ERR_ARG;
+          stk_off[i] = elems;
+          elems += 1ull << (lgp + ri);
+        }
+        lgp += ri;
+      }
+      if (hipMalloc(&d_stk_tab, elems * SCRW * 4) != hipSuccess) return NTT_ERR_HIP;
+      for (auto*& p : d_stk_buf)
+        if (hipMalloc(&p, (size_t)n * MEMW * 4) != hipSuccess) return NTT_ERR_HIP;
+      lgp = r[stk_ord[0]];
+      for (unsigned i = 1; i < npass; ++i) {
+        const unsigned ri = r[stk_ord[i]];
+        if (launch_build_tw<E>(d_stk_tab + stk_off[i] * SCRW, 1ull << (lgp + ri), ri, tl - ri, log_n - lgp - ri,
+                               d_tab + off_los_f, d_tab + off_hi_f, lo_bits, Ff, nullptr) != hipSuccess)
+          return NTT_ERR_HIP;
+        lgp += ri;
+      }
+      return hipDeviceSynchronize() == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+    }
+  }
+
+  int run_stockham(const uint32_t* in, uint32_t* out, hipStream_t st) {
+    const uint32_t grid = (uint32_t)(n >> tile_log_of<E>());
+    hipError_t e = hipSuccess;
+    unsigned lgp = 0;
+    begin(st);
+    for (unsigned i = 0; i < npass && e == hipSuccess; ++i) {
+      const unsigned ri = r[stk_ord[i]];
+      PassArgs<E> A = base_args(false);
+      A.tw_int = d_tab + off_int_f[stk_ord[i]];  // w_R^e for this pass's radix
+      A.tw_full = i ? d_stk_tab + stk_off[i] * SCRW : nullptr;
+      A.log_blk = log_n;
+      A.lgp = lgp;
+      A.src_user = 1;
+      const uint32_t* src = i == 0 ? in : d_stk_buf[(i - 1) & 1];
+      uint32_t* dst = i + 1 == npass ? out : d_stk_buf[i & 1];
+      e = launch_pass<E>(KIND_STOCKHAM, (int)ri, src, dst, A, grid, 1, st);
+      mark(st);
+      lgp += ri;
+    }
+    return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
   }
 
   // Full per-pass outer-twiddle tables: pass i needs N_i entries (N_1 = n, N_2 = n / R_1, ...),
@@ -672,6 +740,8 @@ struct PlanImpl final : PlanBase {
 
   int run(void* d, unsigned batch, bool inverse, hipStream_t st) override {
     if (!d || batch == 0 || (flags & NTT_PLAN_TWIDDLE_ONLY)) return NTT_ERR_ARG;
+    if ((flags & NTT_PLAN_STOCKHAM) && !inverse && batch == 1 && d_stk_tab)
+      return run_stockham(static_cast<uint32_t*>(d), static_cast<uint32_t*>(d), st);
     return run_io(static_cast<uint32_t*>(d), nullptr, static_cast<uint32_t*>(d), batch, inverse, st);
   }
 

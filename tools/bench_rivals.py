@@ -1,0 +1,55 @@
+"""Default four-step DIF schedule vs the rival schedule (the reference's bellperson / improved_NTT
+family as Stockham autosort passes, NTT_PLAN_STOCKHAM): forward transforms, inputs in HBM.
+
+    python tools/bench_rivals.py [--out gpurun_out/rivals.jsonl]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fn, warmup=40, steps=40):
+    import torch
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default="gpurun_out/rivals.jsonl")
+    args = ap.parse_args()
+    import torch
+    from ntt_amd.ntt import NTTPlan
+    rows = []
+    for fid, L, lg in ((1, 4, 24), (1, 4, 20), (0, 1, 24), (0, 1, 26)):
+        for sched in ("default", "stockham"):
+            pl = NTTPlan(fid, lg, L, stockham=(sched == "stockham"))
+            t = pl.fill(pl.empty(), "random", seed=1)
+            pl.set_profiling(True)
+            s = timeit(lambda: pl.forward(t))
+            launches = pl.last_launch_ms()
+            pl.set_profiling(False)
+            r = {"field": fid, "limbs64": L, "log_n": lg, "schedule": sched, "passes": pl.passes, "ms": s * 1e3,
+                 "elements_per_s": (1 << lg) / s, "launch_ms": launches}
+            rows.append(r)
+            print(json.dumps(r), flush=True)
+            del pl, t
+            torch.cuda.empty_cache()
+    os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
+    with open(args.out, "w") as f:
+        for r in rows:
+            f.write(json.dumps(r) + "\n")
+
+
+if __name__ == "__main__":
+    main()
