@@ -175,18 +175,22 @@ def main():
     n = 1 << args.log_n
 
     use_dist = world > 1 or four_step
+    # NTT_BENCH_EXCHANGE=host: rehearsal of N ranks on ONE GPU (RCCL refuses duplicate devices): the
+    # all-to-all is staged through host memory over gloo.  Not a measurement of the product path.
+    rehearsal = os.environ.get("NTT_BENCH_EXCHANGE", "") == "host"
     if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29512")
         os.environ.setdefault("RANK", "0")
         os.environ.setdefault("WORLD_SIZE", "1")
-        if four_step:  # the data path exchanges over RCCL (all-to-all)
+        if four_step and not rehearsal:  # the data path exchanges over RCCL (all-to-all)
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-        else:  # independent transforms: the only collectives are the timing barrier and max
+        else:  # independent transforms (or the rehearsal): barrier / max / host exchange over gloo
             dist.init_process_group("gloo")
     if four_step:
         from ntt_amd.distributed import DistNTT
-        eng = DistNTT(field_id=args.field, log_n=args.log_n, limbs64=args.limbs, device=local)
+        eng = DistNTT(field_id=args.field, log_n=args.log_n, limbs64=args.limbs, device=local,
+                      host_exchange=rehearsal)
         data = eng.empty()
         eng.fill(data, "random", seed=2)
         step = (lambda: eng.inverse(data)) if args.inverse else (lambda: eng.forward(data))
@@ -223,7 +227,7 @@ def main():
 
     elapsed = t1 - t0
     if use_dist:
-        dev = f"cuda:{local}" if four_step else "cpu"
+        dev = f"cuda:{local}" if (four_step and not rehearsal) else "cpu"
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
@@ -254,7 +258,9 @@ def main():
                                f"{FIELD_NAMES[args.field]}, {args.limbs}x64-bit limbs, natural order, in place",
                    "log_n": args.log_n, "field": FIELD_NAMES[args.field], "limbs64": args.limbs,
                    "passes_log_radix": passes,
-                   "parallelism": (f"four-step over {world} GPU(s) (RCCL all-to-all, one transform)" if four_step
+                   "parallelism": ((f"REHEARSAL: four-step over {world} ranks, host-staged gloo exchange"
+                                    if rehearsal else
+                                    f"four-step over {world} GPU(s) (RCCL all-to-all, one transform)") if four_step
                                    else ("single GPU" if world == 1 else
                                          f"{world} GPUs, one independent transform per rank (no data-path "
                                          f"collective)")),

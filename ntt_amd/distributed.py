@@ -214,10 +214,13 @@ class DistNTT:
     """
 
     def __init__(self, field_id: int = 1, log_n: int = 24, limbs64: int = 4, device: Optional[int] = None,
-                 group=None):
+                 group=None, host_exchange: bool = False):
+        """host_exchange: stage the all-to-all through host memory over a gloo group (rehearsing
+        several ranks on ONE GPU, where RCCL refuses duplicate devices); never the product path."""
         import torch.distributed as dist
         self.dist = dist
         self.group = group
+        self.host_exchange = host_exchange
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
         if device is None:
@@ -237,6 +240,11 @@ class DistNTT:
     def _exchange(self, send, recv):
         s, r = send.view(-1), recv.view(-1)
         world = self.layout.world
+        if self.host_exchange:
+            hr = torch.empty(r.shape, dtype=r.dtype)
+            self.dist.all_to_all_single(hr, s.cpu(), group=self.group)
+            r.copy_(hr)
+            return
         per = s.numel() // world  # int64 words per peer
         if per * 8 <= self.MAX_PEER_BYTES:
             self.dist.all_to_all_single(r, s, group=self.group)

@@ -134,3 +134,58 @@ def test_twiddle_pack_and_transpose_building_blocks(fid, L):
         for c_ in range(1 << lcols):
             srow = (r_ >> lbr) * bs + (r_ & ((1 << lbr) - 1)) * (1 << lcols) + c_
             assert torch.equal(o[c_, r_], s2[srow])
+
+
+def _dist_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+    from ntt_amd.distributed import DistNTT
+    from ntt_amd.ntt import NTTPlan
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        log_n = 16
+        d = DistNTT(1, log_n, 4, device=0, host_exchange=True)
+        x = d.fill(d.empty(), "random", seed=8)
+        x0 = x.clone()
+        d.forward(x)
+        ref = NTTPlan(1, log_n, 4)
+        X = ref.fill(ref.empty(), "random", seed=8)
+        ref.forward(X)
+        ok_f = torch.equal(x, X[_index(d.layout, "col")])
+        d.inverse(x)
+        ok_i = torch.equal(x, x0)
+        a, b, c = d.fill(d.empty(), "random", seed=5), d.fill(d.empty(), "random", seed=6), d.empty()
+        d.polymul(a, b, c)
+        A, B, C = ref.fill(ref.empty(), "random", seed=5), ref.fill(ref.empty(), "random", seed=6), ref.empty()
+        ref.polymul(A, B, C)
+        ok_p = torch.equal(c, C[_index(d.layout, "row")])
+        q.put((rank, ok_f, ok_i, ok_p))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, repr(e), False, False))
+
+
+def test_dist_ntt_two_processes_host_exchange():
+    """DistNTT in two processes (ranks 0 and 1 of one transform) on one GPU: rank plans, layouts
+    and the exchange schedule of the N > 1 bench path, with the all-to-all staged through host
+    memory over gloo (RCCL refuses two ranks on one device).  Forward / inverse / polymul bit-exact
+    against the single-GPU transform."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dist_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] is True and r[2] and r[3] for r in res), res
