@@ -75,6 +75,9 @@ struct Eng29 {
   static constexpr bool LDS_SPLIT = false;
   static constexpr int MIN_COLS_LOG = 2;  // column passes own >= 4 adjacent columns: >= 128-B runs
   static constexpr bool PASS1_FULL_TABLE = NTT_256_PASS1_TABLE;  // VALU-bound: a table read beats a second product
+  // column passes after the first take their outer twiddles as Shoup pairs (w, ws) from L2-resident
+  // tables (E::TW words per entry): 143 MADs per product instead of the Montgomery product's 162
+  static constexpr bool SHOUP_OUTER = (L == 9);
   // quotient-estimate reduction needs p's top limb >= 2^18: possible only when 29L - 18 <= 255
   static constexpr bool FASTRED = 29 * L - 18 <= 255;
   struct Tw {
@@ -272,6 +275,7 @@ struct Eng32 {
   // HBM-bound at 1 limb: pass 1 takes its outer twiddles from the two-level tables (2 cheap
   // products) instead of streaming an n-entry table (+50 % pass-1 traffic)
   static constexpr bool PASS1_FULL_TABLE = (N == 1) ? NTT_P_PASS1_TABLE : true;
+  static constexpr bool SHOUP_OUTER = false;
   static constexpr int WAVES_PER_EU = 4;
   static constexpr bool LDS_SPLIT = false;
   struct Tw {

@@ -76,6 +76,8 @@ struct PassArgs {
   uint64_t map_ps;
   const uint32_t* tw_epi;  // final pass: multiply output k of transform b by this table's entry (w R_e,
                            // E::SCRW words; index b N + k in Mode B, k 2^il + b in Mode I) or null
+  uint32_t tw_sh;          // column pass: tw_full holds Shoup pairs (canonical w, floor(w B / p); E::TW words
+                           // per entry, E::SHOUP_OUTER engines) instead of w R_e in the element format
 };
 enum : uint32_t { FS_MAP_IN = 1u, FS_MAP_OUT = 2u, FS_IL = 4u };
 
@@ -89,6 +91,12 @@ template <class E>
 hipError_t launch_build_tw(uint32_t* out, size_t count, uint32_t log_r, uint32_t log_t, uint32_t log_m,
                            const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits, const typename E::Args& F,
                            hipStream_t st, const uint32_t* clo = nullptr, const uint32_t* chi = nullptr);
+// The same table as Shoup pairs (w, floor(w B / p)) in the engine's twiddle format (E::TW words per
+// entry); pinvB = p^-1 mod B (E::W limbs, device memory).  E::SHOUP_OUTER engines only.
+template <class E>
+hipError_t launch_build_tw_sh(uint32_t* out, size_t count, uint32_t log_r, uint32_t log_t, uint32_t log_m,
+                              const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits, const typename E::Args& F,
+                              const uint32_t* pinvB, hipStream_t st);
 template <class E>
 hipError_t launch_build_fs_tw(uint32_t* out, uint32_t log_rows, uint32_t log_cols, uint64_t row0, uint64_t col0,
                               uint32_t log_n, const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits,

@@ -231,8 +231,9 @@ __device__ __forceinline__ void substage(uint32_t (&x)[E::EPT][E::W], uint32_t (
 enum : int { PRO_NONE = 0, PRO_PW = 1, PRO_COSET = 2 };
 // FSM: four-step addressing (PassArgs::fs) compiled in: 0 = plain batched transforms (every
 // product path), 1 = chunk maps / interleave, 2 = the same plus the output twiddle epilogue.
+// SHTW: the column pass's full outer-twiddle table holds Shoup pairs (PassArgs::tw_sh).
 template <class E, int LOGR, int KIND, bool FULLTW, bool FAST, int PRO = PRO_NONE, bool SRC_USER = true,
-          int FSM = 0>
+          int FSM = 0, bool SHTW = false>
 __global__ __launch_bounds__((1 << E::TILE_LOG) / E::EPT) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
 void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                               const PassArgs<E> A) {
@@ -433,8 +434,14 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
               const uint32_t tc = (col0 + c) >> A.il;
               ti = ((size_t)(tc & ~(uint32_t)(T - 1)) << LOGR) + kn * T + (tc & (T - 1));
             }
-            E::template load<E::SCRW>(tw, A.tw_full, NTT_NOMEM(ti));
-            E::mulv(v, tw, A.F);
+            if constexpr (SHTW) {  // Shoup pair (w, floor(w B / p)), E::TW words: 143 MADs, no R_e
+              typename E::Tw tws;
+              E::tload(tws, A.tw_full, NTT_NOMEM(ti));
+              E::mul(v, tws, A.F);
+            } else {
+              E::template load<E::SCRW>(tw, A.tw_full, NTT_NOMEM(ti));
+              E::mulv(v, tw, A.F);
+            }
           } else {
             // outer twiddle w_{N_i}^{col * kn} = w_n^{(col * kn) << log_m} from the two-level
             // tables: t = (lo R_e) * hi, then the Montgomery product v * t / R_e = v * lo * hi
@@ -546,6 +553,58 @@ hipError_t launch_build_tw(uint32_t* out, size_t count, uint32_t log_r, uint32_t
   hipLaunchKernelGGL((k_build_tw<E>), dim3((uint32_t)((count + 255) / 256)), dim3(256), 0, st, out, count, log_r,
                      log_t, log_m, lo, hi, lo_bits, F, clo, chi);
   return hipGetLastError();
+}
+
+// k_build_tw's table as Shoup pairs: entry (c, k) = (w, floor(w B / p)) with w = w_n^((c*k) << log_m)
+// canonical, in the engine's twiddle format (E::TW words).  t = lo_s * hi = w B mod p; w = t / B
+// (Montgomery product by 1); floor(w B / p) = (-(w B mod p)) p^-1 mod B (shoup_ws29).
+template <class E>
+__global__ void k_build_tw_sh(uint32_t* __restrict__ out, size_t count, uint32_t log_r, uint32_t log_t,
+                              uint32_t log_m, const uint32_t* __restrict__ lo, const uint32_t* __restrict__ hi,
+                              uint32_t lo_bits, const typename E::Args F, const uint32_t* __restrict__ pinvB) {
+  constexpr int L = E::W;
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= count) return;
+  const size_t k = (idx >> log_t) & ((1ull << log_r) - 1);
+  const size_t c = ((idx >> (log_t + log_r)) << log_t) + (idx & ((1ull << log_t) - 1));
+  const size_t e = (c * k) << log_m;
+  typename E::Tw a, b;
+  E::tload(a, lo, (uint32_t)(e & ((1ull << lo_bits) - 1)));
+  E::tload(b, hi, (uint32_t)(e >> lo_bits));
+  E::mul(a.w, b, F);  // w B mod p, < 3p
+  uint32_t wr[L], w[L], one[L], t[L], ws[L], pib[L];
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+    wr[i] = a.w[i];
+    one[i] = i == 0 ? 1u : 0u;
+    pib[i] = pinvB[i];
+  }
+  E::template reduce<4, 1, false>(wr, F);  // canonical w B mod p
+#pragma unroll
+  for (int i = 0; i < L; ++i) w[i] = wr[i];
+  E::mulv(w, one, F);  // w, < 3p
+  E::template reduce<4, 1, false>(w, F);
+  neg29<L>(t, wr);
+  mullo29<L>(ws, t, pib);
+  uint32_t o[E::TW];
+#pragma unroll
+  for (int i = 0; i < E::TW; ++i) o[i] = i < L ? w[i] : (i < 2 * L ? ws[i - L] : 0u);
+  uint4* p = reinterpret_cast<uint4*>(out + idx * E::TW);
+#pragma unroll
+  for (int q = 0; q < E::TW / 4; ++q) p[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+}
+
+template <class E>
+hipError_t launch_build_tw_sh(uint32_t* out, size_t count, uint32_t log_r, uint32_t log_t, uint32_t log_m,
+                              const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits, const typename E::Args& F,
+                              const uint32_t* pinvB, hipStream_t st) {
+  if constexpr (!E::SHOUP_OUTER) {
+    return hipErrorInvalidValue;
+  } else {
+    hipLaunchKernelGGL((k_build_tw_sh<E>), dim3((uint32_t)((count + 255) / 256)), dim3(256), 0, st, out, count,
+                       log_r, log_t, log_m, lo, hi, lo_bits, F, pinvB);
+    return hipGetLastError();
+  }
 }
 
 // Four-step twiddle table of one rank (ntt_rplan): entry (a, b) at a 2^log_cols + b holds
@@ -814,6 +873,15 @@ hipError_t launch_count_noncanonical(const uint32_t* d, size_t n, const ModWords
 template <class E, int LOGR, int KIND, bool FULLTW, bool FAST, int FSM>
 static hipError_t launch_plain(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, dim3 g, dim3 b,
                                hipStream_t st) {
+  if constexpr (KIND == KIND_COLUMN && FULLTW && FAST && E::SHOUP_OUTER) {
+    if (A.tw_sh) {  // later column passes: Shoup-pair outer twiddles (they read scratch)
+      if (A.src_user) return hipErrorInvalidValue;
+      constexpr bool SU = E::SCRW == E::MEMW;  // one instance when scratch and caller layouts agree
+      hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true, true, PRO_NONE, SU, FSM, true>), g, b, 0, st, src, dst, A);
+      return hipGetLastError();
+    }
+  }
+  if (A.tw_sh) return hipErrorInvalidValue;
   if constexpr (KIND == KIND_COLUMN && E::SCRW != E::MEMW) {
     if (!A.src_user) {
       hipLaunchKernelGGL((k_pass<E, LOGR, KIND, FULLTW, FAST, PRO_NONE, false, FSM>), g, b, 0, st, src, dst, A);
@@ -971,6 +1039,9 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
   template hipError_t launch_build_tw<E>(uint32_t*, size_t, uint32_t, uint32_t, uint32_t, const uint32_t*,        \
                                          const uint32_t*, uint32_t, const typename E::Args&, hipStream_t,          \
                                          const uint32_t*, const uint32_t*);                                        \
+  template hipError_t launch_build_tw_sh<E>(uint32_t*, size_t, uint32_t, uint32_t, uint32_t, const uint32_t*,     \
+                                            const uint32_t*, uint32_t, const typename E::Args&, const uint32_t*,  \
+                                            hipStream_t);                                                         \
   template hipError_t launch_build_fs_tw<E>(uint32_t*, uint32_t, uint32_t, uint64_t, uint64_t, uint32_t,           \
                                             const uint32_t*, const uint32_t*, uint32_t, const typename E::Args&,    \
                                             hipStream_t);                                                           \

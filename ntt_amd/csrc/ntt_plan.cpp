@@ -15,6 +15,7 @@
 #include <array>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -295,6 +296,10 @@ struct PlanImpl final : PlanBase {
   uint32_t* d_full = nullptr;  // per-pass outer twiddle tables (w R_e, HBM element format), both directions
   size_t full_off[2][8] = {};  // element offsets into d_full, [dir][pass]
   bool use_full = false;
+  uint32_t* d_full_sh = nullptr;  // passes >= 2: the same tables as Shoup pairs (E::TW words per entry)
+  size_t full_sh_off[2][8] = {};  // entry offsets into d_full_sh, [dir][pass]
+  bool full_sh_ok[8] = {};         // pass i takes its outer twiddles from d_full_sh
+  size_t off_pinvB = 0;           // p^-1 mod B (E::W limbs) in d_tab (Shoup-pair table build)
   size_t scratch_elems = 0;
   // table word offsets
   size_t off_int_f[8] = {0}, off_int_i[8] = {0};
@@ -317,6 +322,7 @@ struct PlanImpl final : PlanBase {
     if (d_tab) hipFree(d_tab);
     if (d_scratch) hipFree(d_scratch);
     if (d_full) hipFree(d_full);
+    if (d_full_sh) hipFree(d_full_sh);
     if (d_full_pm) hipFree(d_full_pm);
     if (d_stk_tab) hipFree(d_stk_tab);
     for (auto* p : d_stk_buf)
@@ -478,6 +484,11 @@ struct PlanImpl final : PlanBase {
       host.insert(host.end(), enc, enc + TW);
       while (host.size() % 4) host.push_back(0);
     }
+    if constexpr (E::SHOUP_OUTER) {
+      off_pinvB = host.size();
+      host.insert(host.end(), EH.pinvB, EH.pinvB + E::W);
+      while (host.size() % 4) host.push_back(0);
+    }
     pm2_ = pm2;
     int cur = 0;
     hipGetDevice(&cur);
@@ -585,7 +596,53 @@ struct PlanImpl final : PlanBase {
     }
     if (hipDeviceSynchronize() != hipSuccess) return NTT_ERR_HIP;
     use_full = true;
-    return NTT_OK;
+    return build_shoup_tables();
+  }
+
+  // Column passes 2..p-1 whose table is small enough to stay in L2 (N_i entries of E::TW words <=
+  // 8 MiB): Shoup pairs instead of w R_e, so their outer-twiddle product is a Shoup product (143
+  // MADs) instead of a Montgomery one (162).  Measured (profiles/r02_sh/): 2^24 pass 2 (5 MiB table)
+  // -0.5 %, 2^28 pass 3 (1.3 MiB) -1.2 %, 2^28 pass 2 (168 MiB, not L2-resident) +6 % -- hence the cap.
+  // NTT_SHOUP_OUTER=0 in the environment keeps the Montgomery tables (A/B switch).
+  int build_shoup_tables() {
+    if constexpr (!E::SHOUP_OUTER) {
+      return NTT_OK;
+    } else {
+      if (const char* v = getenv("NTT_SHOUP_OUTER"); v && v[0] == '0') return NTT_OK;
+      if (npass < 3 || !Ff.red_ok) return NTT_OK;  // the Shoup-pair column kernels are FAST instances
+      constexpr size_t kMaxTableBytes = 8ull << 20;
+      size_t elems = 0;
+      unsigned blk = log_n - r[0];
+      for (unsigned i = 1; i + 1 < npass; ++i) {
+        full_sh_off[0][i] = elems;
+        full_sh_ok[i] = ((1ull << blk) * TW * 4) <= kMaxTableBytes;
+        if (full_sh_ok[i]) elems += 1ull << blk;
+        blk -= r[i];
+      }
+      if (elems == 0) return NTT_OK;
+      size_t free_b = 0, total_b = 0;
+      if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return NTT_OK;
+      if (2 * elems * TW * 4 > free_b / 8) return NTT_OK;
+      if (hipMalloc(&d_full_sh, 2 * elems * TW * 4) != hipSuccess) return NTT_ERR_HIP;
+      for (int dir = 0; dir < 2; ++dir) {
+        blk = log_n - r[0];
+        for (unsigned i = 1; i + 1 < npass; ++i) {
+          full_sh_off[dir][i] = dir * elems + full_sh_off[0][i];
+          if (!full_sh_ok[i]) {
+            blk -= r[i];
+            continue;
+          }
+          const uint32_t* lo = d_tab + (dir ? off_los_i : off_los_f);
+          const uint32_t* hi = d_tab + (dir ? off_hi_i : off_hi_f);
+          if (launch_build_tw_sh<E>(d_full_sh + full_sh_off[dir][i] * TW, 1ull << blk, r[i], tile_log_of<E>() - r[i],
+                                    log_n - blk, lo, hi, lo_bits, dir ? Fi : Ff, d_tab + off_pinvB,
+                                    nullptr) != hipSuccess)
+            return NTT_ERR_HIP;
+          blk -= r[i];
+        }
+      }
+      return hipDeviceSynchronize() == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+    }
   }
 
   // Append count entries base^k * scale (engine table format) to host; returns their word offset.
@@ -794,6 +851,10 @@ struct PlanImpl final : PlanBase {
         // pass 1 of a memory-bound engine (8-B P path) computes its outer twiddles from the
         // L2-resident two-level tables: two 32-bit products are cheaper than streaming an n-entry table
         A.tw_full = (use_full && (i > 0 || E::PASS1_FULL_TABLE)) ? d_full + full_off[inverse ? 1 : 0][i] * SCRW : nullptr;
+        if (i > 0 && d_full_sh && full_sh_ok[i]) {
+          A.tw_full = d_full_sh + full_sh_off[inverse ? 1 : 0][i] * TW;
+          A.tw_sh = 1;
+        }
         if (i == 0 && in2) {
           A.src2 = in2;
           A.tw_full = d_full_pm;
