@@ -125,14 +125,31 @@ struct Eng29 {
   // p_top >= 2^18; it is one less only when x / p is within ~2^-14 below an integer, so the result
   // is < p for all but ~2^-14 of inputs.  x - q p = (x + q pbar) mod B.  9 MADs + ~30 simple ops
   // instead of up to four conditional subtractions.
+  // The carry stays 32-bit: q <= 64 and pbar_i < 2^29, so every column is < 2^35.2 and its carry
+  // c < 2^6.2; x_i + c < 2^32 for the input limbs (< 2^31.6).  Per limb one 32-bit add, one MAD
+  // (q pbar_i + (x_i + c)), a mask and one v_alignbit (the carry) -- instead of a 64-bit shift and a
+  // 64-bit add of the zero-extended limb, whose register pairs cost the compiler extra moves.
+  // R32 = false: the 64-bit-carry form, which needs fewer registers (the column passes run at the
+  // 128-VGPR cap, where the 32-bit form spills and measured 3.6 % slower in pass 1).
+  template <bool R32 = true>
   __device__ static __forceinline__ void reduce_top(uint32_t (&x)[W], const Args& A) {
     const float qf = __builtin_fmaf((float)x[L - 1], A.red_inv, -0x1p-15f);
     const uint32_t q = qf > 0.f ? (uint32_t)qf : 0u;
+    if constexpr (R32) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+      const uint64_t acc = (uint64_t)q * A.pbar[i] + (uint32_t)(x[i] + c);
+      x[i] = (uint32_t)acc & kMask29;
+      c = (uint32_t)(acc >> 29);
+    }
+    } else {
     uint64_t acc = 0;
 #pragma unroll
     for (int i = 0; i < L; ++i) {
       acc = (acc >> 29) + x[i] + (uint64_t)q * A.pbar[i];
       x[i] = (uint32_t)acc & kMask29;
+    }
     }
   }
   // FAST (a kernel template flag, chosen per plan from Args::red_ok): quotient-estimate reduction
@@ -143,10 +160,10 @@ struct Eng29 {
   __device__ static __forceinline__ void cond_sub_rare(uint32_t (&x)[W], const uint32_t (&q)[L]) {
     if (__any(x[L - 1] >= q[L - 1])) cond_sub<L>(x, q);
   }
-  template <int FROM, int TO, bool FAST = false>
+  template <int FROM, int TO, bool FAST = false, bool R32 = true>
   __device__ static __forceinline__ void reduce(uint32_t (&x)[W], const Args& A) {
     if constexpr (FAST && FROM > 4 && TO <= 4) {
-      reduce_top(x, A);
+      reduce_top<R32>(x, A);
       if constexpr (TO == 1) cond_sub_rare(x, A.kp[0]);
     } else if constexpr (FAST && FROM == 4 && TO == 2) {
       cond_sub_rare(x, A.kp[1]);  // products: < 1.6p for BN254 Fr, < 2.4p for BLS12-381 Fr
@@ -200,6 +217,17 @@ struct Eng29 {
 #pragma unroll
     for (int i = 0; i < W; ++i) x[i] = r[i];
   }
+  // the same product by a wave-uniform twiddle (the w_8^k constants of the in-register DFTs): its
+  // words stay in SGPRs instead of being copied to VGPRs before every product
+  __device__ static __forceinline__ void mul_u(uint32_t (&x)[W], const Tw& t, const Args& A) {
+    uint32_t r[W];
+    if constexpr (L == 9)
+      mulc29_a9u(r, x, t.w, t.ws, A.pbar);
+    else
+      mulc29_blk<L>(r, x, t.w, t.ws, A.pbar);
+#pragma unroll
+    for (int i = 0; i < W; ++i) x[i] = r[i];
+  }
   // x <- x * y / B mod p (Montgomery product of two variables), x < 32p, y < 4p: result < 3p
   __device__ static __forceinline__ void mulv(uint32_t (&x)[W], const uint32_t (&y)[W], const Args& A) {
     uint32_t r[W];
@@ -230,7 +258,7 @@ struct Eng29 {
   __device__ static __forceinline__ void bfly_w_l(uint32_t (&a)[W], uint32_t (&b)[W], const Tw& t,
                                                   const Args& A) {
     bfly_l<K>(a, b, A);
-    mul(b, t, A);
+    mul_u(b, t, A);  // t: one of the w_8^k kernel arguments
   }
   // ---- unnormalised butterflies (FAST engines; limb/value bounds tracked in dft_q_fast)
   template <int CI>
@@ -246,7 +274,7 @@ struct Eng29 {
   __device__ static __forceinline__ void bfly_raw_w(uint32_t (&a)[W], uint32_t (&b)[W], const Tw& t,
                                                     const Args& A) {
     bfly_raw<CI>(a, b, A);
-    mul(b, t, A);
+    mul_u(b, t, A);  // t: one of the w_8^k kernel arguments
   }
   __device__ static __forceinline__ void norm(uint32_t (&x)[W]) { norm_u<L>(x); }
 };
@@ -303,7 +331,7 @@ struct Eng32 {
     }
   }
   static constexpr bool FASTRED = false;
-  template <int FROM, int TO, bool FAST = false>
+  template <int FROM, int TO, bool FAST = false, bool R32 = true>
   __device__ static __forceinline__ void reduce(uint32_t (&)[W], const Args&) {}
   template <int BOUND, bool FAST = false, int MW = MEMW_>
   __device__ static __forceinline__ void store_lazy(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],

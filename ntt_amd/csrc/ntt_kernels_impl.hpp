@@ -161,13 +161,54 @@ __device__ __forceinline__ void twiddle_mul(uint32_t (&x)[E::W], const uint32_t*
 // LDS slot of (local column/block c, in-column position pi): column-minor like HBM, with c XOR-ed
 // by the low bits of pi so that both lane orders used (c fastest, or pi fastest) hit distinct
 // 16-byte slots (the final pass writes with pi fastest: 8-way conflicts without the swizzle).
+// NTT_LDS_SWZ=1 also XORs pi's low 2 bits with bits 4..5 (tools/lds_sim.py swz_hi: fewer read
+// conflicts for the wave-uniform sub-stage mapping below).
+#ifndef NTT_LDS_SWZ
+#define NTT_LDS_SWZ 0
+#endif
 template <int T>
 __device__ __forceinline__ uint32_t lds_slot(uint32_t c, uint32_t pi) {
-  return (c ^ (pi & (T - 1))) + T * pi;
+  if constexpr (NTT_LDS_SWZ)
+    return (c ^ (pi & (T - 1))) + T * (pi ^ ((pi >> 4) & 3));
+  else
+    return (c ^ (pi & (T - 1))) + T * pi;
+}
+
+// Wave-uniform trivial twiddles.  Sub-stage s multiplies its outputs k = 1..Q-1 by w^(cp k) with
+// cp = g mod sigma_s.  When sigma_s divides the wave count, every cp class is whole waves: wave w
+// takes cp = (w + rot) mod sigma_s (rot = blockIdx.x, so that each SIMD -- which holds the same wave
+// slot of several workgroups -- gets its share of the cp = 0 waves), and the cp = 0 waves skip their
+// products (w^0 = 1) with a scalar branch.  NTT_UNIFORM_CP=0 keeps the lane-order mapping.
+#ifndef NTT_UNIFORM_CP
+#define NTT_UNIFORM_CP 1
+#endif
+template <int LOGR, int QB, int NT, int s>
+struct Uniform {
+  using S = Sched<LOGR, QB>;
+  static constexpr int sb = S::logsig(s);
+  static constexpr bool on = NTT_UNIFORM_CP && s > 0 && s + 1 < S::nsub && sb >= 1 && (1 << sb) <= NT / 64;
+};
+// (local column c, group g) of thread t's j-th group in sub-stage s
+template <int LOGR, int QB, int T, int NT, int EPT, int s>
+__device__ __forceinline__ void sub_map(uint32_t t, int j, uint32_t rot, uint32_t& c, uint32_t& g) {
+  using U = Uniform<LOGR, QB, NT, s>;
+  if constexpr (U::on) {
+    constexpr int sb = U::sb, G = EPT >> Sched<LOGR, QB>::qb(s);
+    const uint32_t wave = t >> 6, lane = t & 63;
+    const uint32_t cp = (wave + rot) & ((1u << sb) - 1);
+    const uint32_t u = ((((wave >> sb) << 6) | lane)) + (uint32_t)(NT >> sb) * (uint32_t)j;
+    (void)G;
+    c = u % T;
+    g = ((u / T) << sb) | cp;
+  } else {
+    const uint32_t lam = t + NT * j;
+    c = lam % T;
+    g = lam / T;
+  }
 }
 
 // One LDS exchange + in-register radix-Q sub-stage s (s >= 1).
-template <class E, int LOGR, int T, int TE, int NT, int s, bool FAST>
+template <class E, int LOGR, int T, int TE, int NT, int s, bool FAST, bool R32>
 __device__ __forceinline__ void substage(uint32_t (&x)[E::EPT][E::W], uint32_t (&cl)[E::EPT / 2],
                                          uint32_t (&pil)[E::EPT / 2], uint32_t* lds, const PassArgs<E>& A, int t) {
   using S = Sched<LOGR, ept_log<E>()>;
@@ -191,8 +232,8 @@ __device__ __forceinline__ void substage(uint32_t (&x)[E::EPT][E::W], uint32_t (
     __syncthreads();
     static_for<G>([&](auto J) {
       constexpr int j = J;
-      const uint32_t lam = t + NT * j;
-      const uint32_t c = lam % T, g = lam / T;
+      uint32_t c, g;
+      sub_map<LOGR, ept_log<E>(), T, NT, EPT, s>(t, j, blockIdx.x, c, g);
       const uint32_t rho = g >> sb, cp = g & ((1u << sb) - 1);
       static_for<Q>([&](auto D) {
         constexpr int d = D;
@@ -203,20 +244,34 @@ __device__ __forceinline__ void substage(uint32_t (&x)[E::EPT][E::W], uint32_t (
   });
   static_for<G>([&](auto J) {
     constexpr int j = J;
-    const uint32_t lam = t + NT * j;
-    cl[j] = lam % T;
-    pil[j] = lam / T;
+    uint32_t c, g;
+    sub_map<LOGR, ept_log<E>(), T, NT, EPT, s>(t, j, blockIdx.x, c, g);
+    cl[j] = c;
+    pil[j] = g;
   });
   static_for<G>([&](auto J) {
     constexpr int j = J;
     dft<E, Q, j * Q, FAST>(x, A.F);
     if constexpr (s + 1 < S::nsub) {
-      E::template reduce<E::IN * Q, E::IN, FAST>(x[j * Q], A.F);  // k = 0: the only output not multiplied
+      E::template reduce<E::IN * Q, E::IN, FAST, R32>(x[j * Q], A.F);  // k = 0: the only output not multiplied
       const uint32_t cp = pil[j] & ((1u << sb) - 1);
-      static_for<Q - 1>([&](auto K1) {
-        constexpr int k = K1 + 1;
-        twiddle_mul<E>(x[j * Q + brev_bits(k, qb)], A.tw_int, (cp * k) << (LOGR - lN), A.F);
-      });
+      auto twiddles = [&]() {
+        static_for<Q - 1>([&](auto K1) {
+          constexpr int k = K1 + 1;
+          twiddle_mul<E>(x[j * Q + brev_bits(k, qb)], A.tw_int, (cp * k) << (LOGR - lN), A.F);
+        });
+      };
+      if constexpr (Uniform<LOGR, ept_log<E>(), NT, s>::on) {
+        if (__builtin_amdgcn_readfirstlane(cp) == 0) {  // wave-uniform: w^0 = 1, only bring the bounds down
+          static_for<Q - 1>([&](auto K1) {
+            E::template reduce<E::IN * Q, E::IN, FAST, R32>(x[j * Q + brev_bits(K1 + 1, qb)], A.F);
+          });
+        } else {
+          twiddles();
+        }
+      } else {
+        twiddles();
+      }
     }
   });
 }
@@ -242,6 +297,7 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
   constexpr bool COLLIKE = KIND == KIND_COLUMN || KIND == KIND_STOCKHAM;  // column-group geometry
   constexpr int TE = (KIND == KIND_SINGLE) ? (1 << LOGR) : (1 << tile_log_of<E>());
   constexpr int T = TE >> LOGR;  // columns (column pass) or blocks (final / single) per workgroup
+  constexpr bool R32 = KIND != KIND_COLUMN;  // reduce_top form (engines.hpp): column passes are at the VGPR cap
   constexpr int NT = TE / EPT;   // threads
   static_assert(LOGR >= QB && T >= 1, "radix");
   __shared__ __attribute__((aligned(16))) uint32_t lds[TE * LdsParts<E::LDSW, E::LDS_SPLIT>::max_words()];
@@ -385,7 +441,7 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
       constexpr int j = J;
       dft<E, Q, j * Q, FAST>(x, A.F);
       if constexpr (S::nsub > 1) {
-        E::template reduce<E::IN * Q, E::IN, FAST>(x[j * Q], A.F);  // k = 0: the only output not multiplied
+        E::template reduce<E::IN * Q, E::IN, FAST, R32>(x[j * Q], A.F);  // k = 0: the only output not multiplied
         static_for<Q - 1>([&](auto K1) {
           constexpr int k = K1 + 1;
           twiddle_mul<E>(x[j * Q + brev_bits(k, qb)], A.tw_int, pil[j] * k, A.F);
@@ -395,11 +451,11 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
   }
 
   // ------------------------------------------------------------------ sub-stages 1..nsub-1 via LDS
-  if constexpr (S::nsub > 1) substage<E, LOGR, T, TE, NT, 1, FAST>(x, cl, pil, lds, A, t);
-  if constexpr (S::nsub > 2) substage<E, LOGR, T, TE, NT, 2, FAST>(x, cl, pil, lds, A, t);
-  if constexpr (S::nsub > 3) substage<E, LOGR, T, TE, NT, 3, FAST>(x, cl, pil, lds, A, t);
-  if constexpr (S::nsub > 4) substage<E, LOGR, T, TE, NT, 4, FAST>(x, cl, pil, lds, A, t);
-  if constexpr (S::nsub > 5) substage<E, LOGR, T, TE, NT, 5, FAST>(x, cl, pil, lds, A, t);
+  if constexpr (S::nsub > 1) substage<E, LOGR, T, TE, NT, 1, FAST, R32>(x, cl, pil, lds, A, t);
+  if constexpr (S::nsub > 2) substage<E, LOGR, T, TE, NT, 2, FAST, R32>(x, cl, pil, lds, A, t);
+  if constexpr (S::nsub > 3) substage<E, LOGR, T, TE, NT, 3, FAST, R32>(x, cl, pil, lds, A, t);
+  if constexpr (S::nsub > 4) substage<E, LOGR, T, TE, NT, 4, FAST, R32>(x, cl, pil, lds, A, t);
+  if constexpr (S::nsub > 5) substage<E, LOGR, T, TE, NT, 5, FAST, R32>(x, cl, pil, lds, A, t);
   static_assert(S::nsub <= 6, "sub-stages");
 
   // ------------------------------------------------------------------ output

@@ -35,16 +35,19 @@ def stmt(pairs, indent="  "):
     return "\n".join(out)
 
 
-def gen_mulc():
+def gen_mulc(uniform=False):
+    """uniform: the twiddle (w, ws) is wave-uniform (the w_8 / w_4 constants): SGPR operands, so the
+    compiler does not copy its 18 words into VGPRs before every product."""
     o = []
-    o.append("__device__ __forceinline__ void mulc29_a9(uint32_t (&r)[9], const uint32_t (&x)[9], const uint32_t (&w)[9],")
+    name = "mulc29_a9u" if uniform else "mulc29_a9"
+    o.append(f"__device__ __forceinline__ void {name}(uint32_t (&r)[9], const uint32_t (&x)[9], const uint32_t (&w)[9],")
     o.append("                                          const uint32_t (&ws)[9], const uint32_t (&pbar)[9]) {")
     o.append("  uint32_t q[9];")
     o.append("  uint64_t acc = 0, cc;")
     o.append("  // q = floor(x * ws / B) from columns >= 7 (see mulc29)")
     for K in range(L - 2, 2 * L - 1):
         lo, hi = max(0, K - (L - 1)), min(K, L - 1)
-        pairs = [(f"x[{i}]", f"ws[{K - i}]", False) for i in range(lo, hi + 1)]
+        pairs = [(f"x[{i}]", f"ws[{K - i}]", uniform) for i in range(lo, hi + 1)]
         o.append(stmt(pairs))
         if K >= L:
             o.append(f"  q[{K - L}] = (uint32_t)acc & kMask29;")
@@ -53,7 +56,7 @@ def gen_mulc():
     o.append("  acc = 0;")
     o.append("  // r = (x * w + q * pbar) mod B")
     for K in range(L):
-        pairs = [(f"x[{i}]", f"w[{K - i}]", False) for i in range(K + 1)]
+        pairs = [(f"x[{i}]", f"w[{K - i}]", uniform) for i in range(K + 1)]
         pairs += [(f"q[{i}]", f"pbar[{K - i}]", True) for i in range(K + 1)]
         o.append(stmt(pairs))
         o.append(f"  r[{K}] = (uint32_t)acc & kMask29;")
@@ -191,14 +194,24 @@ def main():
     print(gen_mulc_whole())
     print()
     print(gen_mont_whole())
+    print("__device__ __forceinline__ void mulc29_a9u(uint32_t (&r)[9], const uint32_t (&x)[9], const uint32_t (&w)[9],")
+    print("                                           const uint32_t (&ws)[9], const uint32_t (&pbar)[9]) {")
+    print("  mulc29_a9(r, x, w, ws, pbar);")
+    print("}")
     print("#elif defined(__HIP_DEVICE_COMPILE__)")
     print("// one asm statement per product column")
     print(gen_mulc())
+    print()
+    print(gen_mulc(uniform=True))
     print()
     print(gen_mont())
     print("#else  // host pass: the generic forms (same results)")
     print("F29_HD void mulc29_a9(uint32_t (&r)[9], const uint32_t (&x)[9], const uint32_t (&w)[9], const uint32_t (&ws)[9],")
     print("                       const uint32_t (&pbar)[9]) {")
+    print("  mulc29<9>(r, x, w, ws, pbar);")
+    print("}")
+    print("F29_HD void mulc29_a9u(uint32_t (&r)[9], const uint32_t (&x)[9], const uint32_t (&w)[9], const uint32_t (&ws)[9],")
+    print("                        const uint32_t (&pbar)[9]) {")
     print("  mulc29<9>(r, x, w, ws, pbar);")
     print("}")
     print("F29_HD void mont29_a9(uint32_t (&r)[9], const uint32_t (&a)[9], const uint32_t (&b)[9], const Mod29<9>& M) {")
