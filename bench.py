@@ -46,16 +46,22 @@ SHOUP_MADS, MONT_MADS = 143, 162  # v_mad_u64_u32 per 256-bit product (field29.h
 
 
 def pass_mads(log_r: int, column: bool) -> float:
-    """v_mad_u64_u32 per element in one pass of radix 2^log_r (ntt_kernels_impl.hpp, 256-bit class:
-    4 elements per thread): radix-4/2 register sub-stages with 1/4, 0 internal products per element,
-    (Q-1)/Q twiddle products between sub-stages (Shoup), and in column passes one outer-twiddle
-    Montgomery product.  (Quotient-estimate reductions, 9 MADs each, are not counted.)"""
+    """v_mad_u64_u32 issued per element in one pass of radix 2^log_r (ntt_kernels_impl.hpp, 256-bit
+    class: 4 elements per thread, 4 waves per workgroup): radix-4/2 register sub-stages with 1/4, 0
+    internal products per element, (Q-1)/Q twiddle products between sub-stages (Shoup) -- except in
+    the wave-uniform sub-stages (sigma_s = 2^logsig(s) <= 4 waves), whose cp = 0 waves (1/sigma_s of
+    them) skip theirs -- and in column passes one outer-twiddle Montgomery product.
+    (Quotient-estimate reductions, 9 MADs each, are not counted.)"""
     subs, r = [], log_r
     while r > 0:
         subs.append(min(2, r))
         r -= min(2, r)
     internal = {3: 5 / 8, 2: 1 / 4, 1: 0.0}
-    shoup = sum(internal[q] for q in subs) + sum((2 ** q - 1) / 2 ** q for q in subs[:-1])
+    shoup = sum(internal[q] for q in subs)
+    for s, q in enumerate(subs[:-1]):
+        sig = 2 ** (log_r - 2 * s - q)  # sigma_s
+        skip = 1 / sig if (s >= 1 and 2 <= sig <= 4) else 0.0
+        shoup += (2 ** q - 1) / 2 ** q * (1 - skip)
     return shoup * SHOUP_MADS + (MONT_MADS if column else 0)
 FIELD_NAMES = {0: "P469762049", 1: "BN254_FR", 2: "BLS12_381_FR"}
 
@@ -74,6 +80,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--four-step", "--dist", dest="four_step", action="store_true",
                     help="one transform split over all ranks (four-step + RCCL all-to-all); default for N > 1")
+    ap.add_argument("--pieces", type=int, default=4,
+                    help="four-step: row pieces whose all-to-all overlaps the next piece's row transforms")
     ap.add_argument("--independent", action="store_true",
                     help="N > 1: one independent transform per rank (weak scaling, no data-path collective)")
     ap.add_argument("--cpu-log-n", type=int, default=22, help="C-oracle single-core sample size (log2)")
@@ -190,7 +198,7 @@ def main():
     if four_step:
         from ntt_amd.distributed import DistNTT
         eng = DistNTT(field_id=args.field, log_n=args.log_n, limbs64=args.limbs, device=local,
-                      host_exchange=rehearsal)
+                      host_exchange=rehearsal, pieces=args.pieces)
         data = eng.empty()
         eng.fill(data, "random", seed=2)
         step = (lambda: eng.inverse(data)) if args.inverse else (lambda: eng.forward(data))
@@ -264,7 +272,8 @@ def main():
                                    else ("single GPU" if world == 1 else
                                          f"{world} GPUs, one independent transform per rank (no data-path "
                                          f"collective)")),
-                   "transforms_per_step": jobs},
+                   "transforms_per_step": jobs,
+                   **({"exchange_pieces": len(eng.fs.pieces)} if four_step else {})},
     }
     # ---- SURVEY §8(d) roofline of the whole transform: 2 n S algorithmic bytes per transform
     gpus_per_transform = world if four_step else 1

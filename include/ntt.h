@@ -199,6 +199,15 @@ int ntt_rplan_forward_cols(ntt_rplan* rp, const void* d_recv, void* d_x, unsigne
 int ntt_rplan_inverse_cols(ntt_rplan* rp, const void* d_x, const void* d_y, void* d_send, void* hip_stream);
 /* recv (nvec = 1) -> row layout out (1/n included over both halves) */
 int ntt_rplan_inverse_rows(ntt_rplan* rp, const void* d_recv, void* d_out, void* hip_stream);
+/* The same two row steps over local rows [row0, row0 + nrows) only (1 <= nrows, row0 + nrows <= r).
+ * Rows [row0, row0 + nrows) of every peer chunk form the contiguous run
+ * [row0 c, (row0 + nrows) c) of that chunk, so a caller can exchange each piece as soon as it is written
+ * (forward) or transform each piece as soon as it has arrived (inverse): the exchange of one piece
+ * overlaps the row transforms of the next. */
+int ntt_rplan_forward_rows_range(ntt_rplan* rp, const void* d_x, void* d_send, unsigned nvec, unsigned slot,
+                                 uint64_t row0, uint64_t nrows, void* hip_stream);
+int ntt_rplan_inverse_rows_range(ntt_rplan* rp, const void* d_recv, void* d_out, uint64_t row0, uint64_t nrows,
+                                 void* hip_stream);
 /* this rank's row-layout share of the global synthetic vector (kinds as ntt_fill) */
 int ntt_rplan_fill(ntt_rplan* rp, void* d_x, int kind, uint64_t seed, void* hip_stream);
 /* per-launch timing of the row (which = 0) or column (1) transforms, as ntt_plan_last_launch_ms */

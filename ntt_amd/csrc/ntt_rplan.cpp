@@ -65,6 +65,12 @@ hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
 
 bool nvec_ok(unsigned nvec, unsigned slot) { return (nvec == 1 || nvec == 2) && slot < nvec; }
 
+// a row piece [row0, row0 + nrows) of the r local rows
+bool range_ok(const ntt_rplan* rp, uint64_t row0, uint64_t nrows) {
+  const uint64_t r = 1ull << rp->log_r;
+  return nrows >= 1 && row0 < r && nrows <= r - row0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -129,16 +135,25 @@ int ntt_rplan_info(const ntt_rplan* rp, uint64_t* local_n, uint64_t* chunk, unsi
   return NTT_OK;
 }
 
-int ntt_rplan_forward_rows(ntt_rplan* rp, const void* d_x, void* d_send, unsigned nvec, unsigned slot, void* s) {
-  if (!rp || !d_x || !d_send || !nvec_ok(nvec, slot)) return NTT_ERR_ARG;
+int ntt_rplan_forward_rows_range(ntt_rplan* rp, const void* d_x, void* d_send, unsigned nvec, unsigned slot,
+                                 uint64_t row0, uint64_t nrows, void* s) {
+  if (!rp || !d_x || !d_send || !nvec_ok(nvec, slot) || !range_ok(rp, row0, nrows)) return NTT_ERR_ARG;
   DeviceScope scope(rp->device);
+  // batch index b of the launch is local row row0 + b: shift the input rows, the epilogue table rows
+  // and the Mode B output map (row a lands at a c within every peer chunk) by row0
   FsIO io;
   io.fs = FS_MAP_OUT;
   io.map_lc = rp->log_c;
   io.map_ps = nvec * rp->chunk();
-  io.tw_epi = rp->tab_fwd;
-  void* dst = static_cast<char*>(d_send) + slot * rp->chunk() * rp->elem_bytes;
-  return plan_run_fs(rp->rows, d_x, nullptr, dst, 1u << rp->log_r, false, io, S(s));
+  io.tw_epi = static_cast<const char*>(rp->tab_fwd) + (row0 << rp->log_n2) * plan_table_entry_bytes(rp->tw);
+  const void* src = static_cast<const char*>(d_x) + (row0 << rp->log_n2) * rp->elem_bytes;
+  void* dst = static_cast<char*>(d_send) + (slot * rp->chunk() + (row0 << rp->log_c)) * rp->elem_bytes;
+  return plan_run_fs(rp->rows, src, nullptr, dst, (unsigned)nrows, false, io, S(s));
+}
+
+int ntt_rplan_forward_rows(ntt_rplan* rp, const void* d_x, void* d_send, unsigned nvec, unsigned slot, void* s) {
+  if (!rp) return NTT_ERR_ARG;
+  return ntt_rplan_forward_rows_range(rp, d_x, d_send, nvec, slot, 0, 1ull << rp->log_r, s);
 }
 
 int ntt_rplan_forward_cols(ntt_rplan* rp, const void* d_recv, void* d_x, unsigned nvec, unsigned slot, void* s) {
@@ -163,14 +178,22 @@ int ntt_rplan_inverse_cols(ntt_rplan* rp, const void* d_x, const void* d_y, void
   return plan_run_fs(rp->cols, d_x, d_y, d_send, 1, true, io, S(s));
 }
 
-int ntt_rplan_inverse_rows(ntt_rplan* rp, const void* d_recv, void* d_out, void* s) {
-  if (!rp || !d_recv || !d_out) return NTT_ERR_ARG;
+int ntt_rplan_inverse_rows_range(ntt_rplan* rp, const void* d_recv, void* d_out, uint64_t row0, uint64_t nrows,
+                                 void* s) {
+  if (!rp || !d_recv || !d_out || !range_ok(rp, row0, nrows)) return NTT_ERR_ARG;
   DeviceScope scope(rp->device);
   FsIO io;
   io.fs = FS_MAP_IN;
   io.map_lc = rp->log_c;
   io.map_ps = rp->chunk();
-  return plan_run_fs(rp->rows, d_recv, nullptr, d_out, 1u << rp->log_r, true, io, S(s));
+  const void* src = static_cast<const char*>(d_recv) + (row0 << rp->log_c) * rp->elem_bytes;
+  void* dst = static_cast<char*>(d_out) + (row0 << rp->log_n2) * rp->elem_bytes;
+  return plan_run_fs(rp->rows, src, nullptr, dst, (unsigned)nrows, true, io, S(s));
+}
+
+int ntt_rplan_inverse_rows(ntt_rplan* rp, const void* d_recv, void* d_out, void* s) {
+  if (!rp) return NTT_ERR_ARG;
+  return ntt_rplan_inverse_rows_range(rp, d_recv, d_out, 0, 1ull << rp->log_r, s);
 }
 
 int ntt_rplan_fill(ntt_rplan* rp, void* d_x, int kind, uint64_t seed, void* s) {

@@ -69,20 +69,38 @@ class Layout:
 class FourStep:
     """Per-rank four-step schedule over an engine (local compute) and an exchange (all-to-all).
 
-    Engine interface (one rank): ``forward_rows(x, send, nvec, slot)`` (row layout -> peer chunks),
-    ``forward_cols(recv, x, nvec, slot)`` (received chunks -> column layout), ``inverse_cols(x, y,
-    send)`` (column layout, times y if given -> peer chunks), ``inverse_rows(recv, out)`` (-> row
-    layout), ``empty(count)``.  Buffers hold [G][nvec][chunk] elements.  Exchange:
-    ``exchange(send, recv)`` = all-to-all of equal contiguous chunks.
+    Engine interface (one rank): ``forward_rows(x, send, nvec, slot, row0, nrows)`` (rows [row0,
+    row0 + nrows) of the row layout -> their runs of every peer chunk), ``forward_cols(recv, x, nvec,
+    slot)`` (received chunks -> column layout), ``inverse_cols(x, y, send)`` (column layout, times y
+    if given -> peer chunks), ``inverse_rows(recv, out, row0, nrows)`` (-> rows of the row layout),
+    ``empty(count)``.  Buffers hold [G][nvec][r][c] elements (a peer chunk is [r][c]).
+
+    Exchange interface: ``start(send, recv, nvec, row0, nrows)`` moves rows [row0, row0 + nrows) of
+    every peer chunk (all nvec vectors) and returns a handle, ordered after the compute enqueued so
+    far; ``wait(handle)`` orders later compute after it.  A plain callable ``exchange(send, recv)``
+    (one all-to-all of whole chunks) is accepted too and runs the schedule unpipelined.
+
+    With ``pieces`` > 1 the row steps run in pieces of r / pieces rows: the forward exchanges each
+    piece while the row transforms of the next one run, the inverse transforms each piece as soon as
+    it has arrived -- the all-to-all overlaps the local transforms instead of following them.
     """
 
-    def __init__(self, layout: Layout, engine, exchange: Optional[Callable] = None):
+    def __init__(self, layout: Layout, engine, exchange=None, pieces: int = 1):
         self.L = layout
         self.eng = engine
+        if exchange is not None and not hasattr(exchange, "start"):
+            exchange, pieces = _WholeExchange(exchange), 1
         self.exchange = exchange
+        self.pieces = self.piece_ranges(layout.r, pieces)
         self.send = engine.empty(layout.local_n)
         self.recv = engine.empty(layout.local_n)
         self.send2 = self.recv2 = None  # [G][2][chunk]: the polymul's batched exchange, on first use
+
+    @staticmethod
+    def piece_ranges(r: int, pieces: int):
+        k = max(1, min(int(pieces), r))
+        step = -(-r // k)
+        return [(a, min(step, r - a)) for a in range(0, r, step)]
 
     def pair_buffers(self):
         if self.send2 is None:
@@ -91,54 +109,74 @@ class FourStep:
         return self.send2, self.recv2
 
     # ---- forward: row layout -> column layout (in place on x)
-    def forward_phase1(self, x):
-        self.eng.forward_rows(x, self.send, 1, 0)
-        return self.send, self.recv
-
-    def forward_phase2(self, x):
-        self.eng.forward_cols(self.recv, x, 1, 0)
+    def forward_rows_piece(self, x, i, nvec=1, slot=0, send=None):
+        a0, ra = self.pieces[i]
+        self.eng.forward_rows(x, self.send if send is None else send, nvec, slot, a0, ra)
 
     def forward(self, x):
-        self.exchange(*self.forward_phase1(x))
-        self.forward_phase2(x)
+        hs = []
+        for i, (a0, ra) in enumerate(self.pieces):
+            self.forward_rows_piece(x, i)
+            hs.append(self.exchange.start(self.send, self.recv, 1, a0, ra))
+        for h in hs:
+            self.exchange.wait(h)
+        self.eng.forward_cols(self.recv, x, 1, 0)
         return x
 
     # ---- inverse: column layout -> row layout (in place on x, or into out with a pointwise factor y)
-    def inverse_phase1(self, x, y=None):
-        self.eng.inverse_cols(x, y, self.send)
-        return self.send, self.recv
+    def inverse_rows_piece(self, out, i):
+        a0, ra = self.pieces[i]
+        self.eng.inverse_rows(self.recv, out, a0, ra)
 
-    def inverse_phase2(self, out):
-        self.eng.inverse_rows(self.recv, out)
+    def _inverse_tail(self, out):
+        hs = [self.exchange.start(self.send, self.recv, 1, a0, ra) for a0, ra in self.pieces]
+        for i, h in enumerate(hs):
+            self.exchange.wait(h)
+            self.inverse_rows_piece(out, i)
+        return out
 
     def inverse(self, x):
-        self.exchange(*self.inverse_phase1(x))
-        self.inverse_phase2(x)
-        return x
+        self.eng.inverse_cols(x, None, self.send)
+        return self._inverse_tail(x)
 
     # ---- polynomial multiply: row-layout a, b -> row-layout out = a * b (cyclic, length n).
     # a and b are left holding their column-layout forward transforms (unless out aliases them).
-    def polymul_phase1(self, a, b):
-        if a is b:  # squaring: one forward, single-vector exchange
-            return self.forward_phase1(a)
-        send2, recv2 = self.pair_buffers()
-        self.eng.forward_rows(a, send2, 2, 0)
-        self.eng.forward_rows(b, send2, 2, 1)
-        return send2, recv2
-
-    def polymul_phase2(self, a, b):
-        if a is b:
-            self.forward_phase2(a)
-        else:
-            self.eng.forward_cols(self.recv2, a, 2, 0)
-            self.eng.forward_cols(self.recv2, b, 2, 1)
-        return self.inverse_phase1(a, b)
-
     def polymul(self, a, b, out):
-        self.exchange(*self.polymul_phase1(a, b))
-        self.exchange(*self.polymul_phase2(a, b))
-        self.inverse_phase2(out)
-        return out
+        if a is b:  # squaring: one forward, single-vector exchange
+            self.forward(a)
+        else:
+            send2, recv2 = self.pair_buffers()
+            hs = []
+            for i, (a0, ra) in enumerate(self.pieces):
+                self.forward_rows_piece(a, i, 2, 0, send2)
+                self.forward_rows_piece(b, i, 2, 1, send2)
+                hs.append(self.exchange.start(send2, recv2, 2, a0, ra))
+            for h in hs:
+                self.exchange.wait(h)
+            self.eng.forward_cols(recv2, a, 2, 0)
+            self.eng.forward_cols(recv2, b, 2, 1)
+        self.eng.inverse_cols(a, b, self.send)
+        return self._inverse_tail(out)
+
+
+class _WholeExchange:
+    """Adapter for a plain ``exchange(send, recv)`` callable: whole-chunk all-to-all, one piece."""
+
+    def __init__(self, fn):
+        self.fn = fn
+
+    def start(self, send, recv, nvec, row0, nrows):
+        self.fn(send, recv)
+
+    def wait(self, handle):
+        pass
+
+
+def piece_views(buf, world: int, nvec: int, r: int, c: int, row0: int, nrows: int):
+    """[peer][vec] views of rows [row0, row0 + nrows) of a [G][nvec][r][c] exchange buffer: each a
+    contiguous run of nrows * c elements."""
+    b = buf.view(world, nvec, r * c, *buf.shape[1:])
+    return [[b[g, v, row0 * c:(row0 + nrows) * c] for v in range(nvec)] for g in range(world)]
 
 
 class RankPlan:
@@ -173,9 +211,10 @@ class RankPlan:
     def _s(self, t):
         return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
-    def forward_rows(self, x, send, nvec, slot):
-        self._L.check(self.lib.ntt_rplan_forward_rows(self.handle, self._p(x), self._p(send), nvec, slot, self._s(x)),
-                      "ntt_rplan_forward_rows")
+    def forward_rows(self, x, send, nvec, slot, row0=0, nrows=None):
+        nrows = self.layout.r - row0 if nrows is None else nrows
+        self._L.check(self.lib.ntt_rplan_forward_rows_range(self.handle, self._p(x), self._p(send), nvec, slot, row0,
+                                                            nrows, self._s(x)), "ntt_rplan_forward_rows_range")
 
     def forward_cols(self, recv, x, nvec, slot):
         self._L.check(self.lib.ntt_rplan_forward_cols(self.handle, self._p(recv), self._p(x), nvec, slot, self._s(x)),
@@ -185,9 +224,10 @@ class RankPlan:
         self._L.check(self.lib.ntt_rplan_inverse_cols(self.handle, self._p(x), self._p(y), self._p(send), self._s(x)),
                       "ntt_rplan_inverse_cols")
 
-    def inverse_rows(self, recv, out):
-        self._L.check(self.lib.ntt_rplan_inverse_rows(self.handle, self._p(recv), self._p(out), self._s(out)),
-                      "ntt_rplan_inverse_rows")
+    def inverse_rows(self, recv, out, row0=0, nrows=None):
+        nrows = self.layout.r - row0 if nrows is None else nrows
+        self._L.check(self.lib.ntt_rplan_inverse_rows_range(self.handle, self._p(recv), self._p(out), row0, nrows,
+                                                            self._s(out)), "ntt_rplan_inverse_rows_range")
 
     def fill(self, t, kind: str = "random", seed: int = 1):
         k = {"iota": 0, "random": 1}[kind]
@@ -210,11 +250,13 @@ class DistNTT:
 
     The default process group must be initialised (``nccl`` backend = RCCL on ROCm).  ``forward``
     takes this rank's row-layout share and leaves its column-layout share in place; ``inverse`` the
-    reverse.  See module docstring for the layouts.
+    reverse.  See module docstring for the layouts.  The all-to-all runs in ``pieces`` row pieces,
+    each an asynchronous RCCL all-to-all on the communicator's stream, overlapping the row transforms
+    (FourStep).
     """
 
     def __init__(self, field_id: int = 1, log_n: int = 24, limbs64: int = 4, device: Optional[int] = None,
-                 group=None, host_exchange: bool = False):
+                 group=None, host_exchange: bool = False, pieces: int = 4):
         """host_exchange: stage the all-to-all through host memory over a gloo group (rehearsing
         several ranks on ONE GPU, where RCCL refuses duplicate devices); never the product path."""
         import torch.distributed as dist
@@ -229,32 +271,40 @@ class DistNTT:
         self.field_id, self.log_n, self.limbs64 = field_id, log_n, limbs64
         self.layout = Layout(log_n, world, rank)
         self.engine = RankPlan(field_id, log_n, limbs64, world, rank, device)
-        self.fs = FourStep(self.layout, self.engine, self._exchange)
+        self.fs = FourStep(self.layout, self.engine, self, pieces=1 if world == 1 else pieces)
         self.n = self.layout.n
         self.passes: List[int] = []  # per-transform schedules: see the row / column plans
 
     # RCCL moves < 2 GiB per peer per collective (a 2 GiB chunk arrived half copied,
-    # tests/test_gpu_fullsize.py): larger per-peer chunks go as several all-to-alls of pieces.
+    # tests/test_gpu_fullsize.py): larger per-peer runs go as several all-to-alls.
     MAX_PEER_BYTES = 1 << 30
 
-    def _exchange(self, send, recv):
-        s, r = send.view(-1), recv.view(-1)
-        world = self.layout.world
-        if self.host_exchange:
-            hr = torch.empty(r.shape, dtype=r.dtype)
-            self.dist.all_to_all_single(hr, s.cpu(), group=self.group)
-            r.copy_(hr)
-            return
-        per = s.numel() // world  # int64 words per peer
-        if per * 8 <= self.MAX_PEER_BYTES:
-            self.dist.all_to_all_single(r, s, group=self.group)
-            return
-        sv, rv = s.view(world, per), r.view(world, per)
-        piece = self.MAX_PEER_BYTES // 8
-        for off in range(0, per, piece):
-            cnt = min(piece, per - off)
-            self.dist.all_to_all([rv[g, off:off + cnt] for g in range(world)],
-                                 [sv[g, off:off + cnt] for g in range(world)], group=self.group)
+    # ---- FourStep exchange interface: rows [row0, row0 + nrows) of every peer chunk
+    def start(self, send, recv, nvec, row0, nrows):
+        L = self.layout
+        sv = piece_views(send, L.world, nvec, L.r, L.c, row0, nrows)
+        rv = piece_views(recv, L.world, nvec, L.r, L.c, row0, nrows)
+        works = []
+        for v in range(nvec):
+            ins = [sv[g][v] for g in range(L.world)]
+            outs = [rv[g][v] for g in range(L.world)]
+            if self.host_exchange:
+                hr = torch.empty((L.world * ins[0].shape[0],) + tuple(ins[0].shape[1:]), dtype=ins[0].dtype)
+                self.dist.all_to_all_single(hr, torch.cat(ins).cpu(), group=self.group)
+                for g, o in enumerate(outs):
+                    o.copy_(hr[g * o.shape[0]:(g + 1) * o.shape[0]])
+                continue
+            rows_b = ins[0][0:1].numel() * 8  # bytes per element
+            step = max(1, self.MAX_PEER_BYTES // rows_b)
+            for off in range(0, ins[0].shape[0], step):
+                works.append(self.dist.all_to_all([o[off:off + step] for o in outs],
+                                                  [t[off:off + step] for t in ins], group=self.group,
+                                                  async_op=True))
+        return works
+
+    def wait(self, works):
+        for w in works:
+            w.wait()
 
     def empty(self) -> torch.Tensor:
         return self.engine.empty(self.layout.local_n)
@@ -284,22 +334,38 @@ class DistNTT:
 class VirtualRanks:
     """G ranks of the four-step in ONE process on one GPU; the all-to-all is device copies.
 
-    SURVEY §4: validate the distributed decomposition on a single GPU before RCCL.
+    SURVEY §4: validate the distributed decomposition on a single GPU before RCCL.  With ``pieces``
+    > 1 the copies of each row piece run on a side stream while the next piece's row transforms run
+    (the schedule of FourStep, interleaved over the G ranks).
     """
 
-    def __init__(self, field_id: int, log_n: int, limbs64: int, world: int, device: int = 0):
+    def __init__(self, field_id: int, log_n: int, limbs64: int, world: int, device: int = 0, pieces: int = 1):
         self.world = world
         self.engines = [RankPlan(field_id, log_n, limbs64, world, g, device) for g in range(world)]
-        self.ranks = [FourStep(Layout(log_n, world, g), e) for g, e in enumerate(self.engines)]
+        self.ranks = [FourStep(Layout(log_n, world, g), e, pieces=pieces) for g, e in enumerate(self.engines)]
         self.layout0 = self.ranks[0].L
+        self.pieces = self.ranks[0].pieces
+        self.side = torch.cuda.Stream(device=device)
 
-    def _exchange_all(self, bufs):
-        G = self.world
-        sends, recvs = [s for s, _ in bufs], [r for _, r in bufs]
-        chunk = sends[0].shape[0] // G
-        for dst in range(G):
-            for src in range(G):
-                recvs[dst][src * chunk:(src + 1) * chunk].copy_(sends[src][dst * chunk:(dst + 1) * chunk])
+    def _copy_piece(self, sends, recvs, nvec, row0, nrows):
+        """Rows [row0, row0 + nrows) of every (src -> dst) chunk, on the side stream after the work
+        enqueued so far; returns the event that marks their arrival."""
+        L, G = self.layout0, self.world
+        ev = torch.cuda.Event()
+        ev.record()
+        self.side.wait_event(ev)
+        with torch.cuda.stream(self.side):
+            sv = [piece_views(t, G, nvec, L.r, L.c, row0, nrows) for t in sends]
+            rv = [piece_views(t, G, nvec, L.r, L.c, row0, nrows) for t in recvs]
+            for dst in range(G):
+                for src in range(G):
+                    for v in range(nvec):
+                        rv[dst][src][v].copy_(sv[src][dst][v])
+            done = torch.cuda.Event()
+            done.record()
+        for t in list(sends) + list(recvs):  # the side stream uses them: keep the caching allocator honest
+            t.record_stream(self.side)
+        return done
 
     def empty(self) -> List[torch.Tensor]:
         return [e.empty(self.layout0.local_n) for e in self.engines]
@@ -310,23 +376,51 @@ class VirtualRanks:
         return xs
 
     def forward(self, xs: List[torch.Tensor]):
-        self._exchange_all([fs.forward_phase1(x) for fs, x in zip(self.ranks, xs)])
+        evs = []
+        for i, (a0, ra) in enumerate(self.pieces):
+            for fs, x in zip(self.ranks, xs):
+                fs.forward_rows_piece(x, i)
+            evs.append(self._copy_piece([fs.send for fs in self.ranks], [fs.recv for fs in self.ranks], 1, a0, ra))
+        for ev in evs:
+            torch.cuda.current_stream().wait_event(ev)
         for fs, x in zip(self.ranks, xs):
-            fs.forward_phase2(x)
+            fs.eng.forward_cols(fs.recv, x, 1, 0)
         return xs
+
+    def _inverse_tail(self, outs):
+        evs = [self._copy_piece([fs.send for fs in self.ranks], [fs.recv for fs in self.ranks], 1, a0, ra)
+               for a0, ra in self.pieces]
+        for i, ev in enumerate(evs):
+            torch.cuda.current_stream().wait_event(ev)
+            for fs, o in zip(self.ranks, outs):
+                fs.inverse_rows_piece(o, i)
+        return outs
 
     def inverse(self, xs: List[torch.Tensor]):
-        self._exchange_all([fs.inverse_phase1(x) for fs, x in zip(self.ranks, xs)])
         for fs, x in zip(self.ranks, xs):
-            fs.inverse_phase2(x)
-        return xs
+            fs.eng.inverse_cols(x, None, fs.send)
+        return self._inverse_tail(xs)
 
     def polymul(self, As: List[torch.Tensor], Bs: List[torch.Tensor], Outs: List[torch.Tensor]):
-        self._exchange_all([fs.polymul_phase1(a, b) for fs, a, b in zip(self.ranks, As, Bs)])
-        self._exchange_all([fs.polymul_phase2(a, b) for fs, a, b in zip(self.ranks, As, Bs)])
-        for fs, o in zip(self.ranks, Outs):
-            fs.inverse_phase2(o)
-        return Outs
+        if all(a is b for a, b in zip(As, Bs)):
+            self.forward(As)
+        else:
+            pairs = [fs.pair_buffers() for fs in self.ranks]
+            sends, recvs = [p[0] for p in pairs], [p[1] for p in pairs]
+            evs = []
+            for i, (a0, ra) in enumerate(self.pieces):
+                for g, fs in enumerate(self.ranks):
+                    fs.forward_rows_piece(As[g], i, 2, 0, sends[g])
+                    fs.forward_rows_piece(Bs[g], i, 2, 1, sends[g])
+                evs.append(self._copy_piece(sends, recvs, 2, a0, ra))
+            for ev in evs:
+                torch.cuda.current_stream().wait_event(ev)
+            for g, fs in enumerate(self.ranks):
+                fs.eng.forward_cols(recvs[g], As[g], 2, 0)
+                fs.eng.forward_cols(recvs[g], Bs[g], 2, 1)
+        for fs, a, b in zip(self.ranks, As, Bs):
+            fs.eng.inverse_cols(a, b, fs.send)
+        return self._inverse_tail(Outs)
 
 
 class MultiPlan:

@@ -36,11 +36,12 @@ class CpuOracleEngine:
     def _ntt(self, vals, inverse):
         return OC.limbs_to_ints(OC.ntt_mp(OC.ints_to_limbs(vals, self.L), self.p, self.g, inverse))
 
-    def forward_rows(self, x, send, nvec, slot):
+    def forward_rows(self, x, send, nvec, slot, row0=0, nrows=None):
         L, p = self.lay, self.p
+        nrows = L.r - row0 if nrows is None else nrows
         xs = self._ints(x)
         idx, vals = [], []
-        for a in range(L.r):
+        for a in range(row0, row0 + nrows):
             X = self._ntt(xs[a * L.n2:(a + 1) * L.n2], False)
             j1 = L.rank * L.r + a
             for k2 in range(L.n2):
@@ -73,14 +74,40 @@ class CpuOracleEngine:
                 out[j1 * L.c + kc] = v * pow(self.winv, j1 * k2 % self.n, p) % p
         self._put(send, range(L.local_n), out)
 
-    def inverse_rows(self, recv, out):
+    def inverse_rows(self, recv, out, row0=0, nrows=None):
         L = self.lay
+        nrows = L.r - row0 if nrows is None else nrows
         rv = self._ints(recv)
-        res = [0] * L.local_n
-        for a in range(L.r):
+        res = []
+        for a in range(row0, row0 + nrows):
             row = [rv[(k2 // L.c) * L.chunk + a * L.c + (k2 % L.c)] for k2 in range(L.n2)]
-            res[a * L.n2:(a + 1) * L.n2] = self._ntt(row, True)
-        self._put(out, range(L.local_n), res)
+            res += self._ntt(row, True)
+        self._put(out, range(row0 * L.n2, (row0 + nrows) * L.n2), res)
+
+
+class GlooPieceExchange:
+    """FourStep exchange interface over any torch.distributed backend: rows [row0, row0 + nrows) of
+    every peer chunk, one all_to_all_single per vector (synchronous; the handle is unused)."""
+
+    def __init__(self, layout):
+        self.L = layout
+
+    def start(self, send, recv, nvec, row0, nrows):
+        import torch.distributed as dist
+        from ntt_amd.distributed import piece_views
+        L = self.L
+        sv = piece_views(send, L.world, nvec, L.r, L.c, row0, nrows)
+        rv = piece_views(recv, L.world, nvec, L.r, L.c, row0, nrows)
+        for v in range(nvec):
+            ins = torch.cat([sv[g][v] for g in range(L.world)])
+            out = torch.empty_like(ins)
+            dist.all_to_all_single(out, ins)
+            for g in range(L.world):
+                m = rv[g][v].shape[0]
+                rv[g][v].copy_(out[g * m:(g + 1) * m])
+
+    def wait(self, handle):
+        pass
 
 
 def row_shares(x_ints, layout_cls, log_n, world, L):

@@ -21,7 +21,15 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, field_id, log_n, L, q):
+def _exchange(layout, pieces):
+    """Whole-chunk all-to-all (plain callable, one piece) or the row-piece exchange interface."""
+    from tests.dist_helpers import GlooPieceExchange
+    if pieces == 1:
+        return lambda s, r: dist.all_to_all_single(r.view(-1), s.view(-1))
+    return GlooPieceExchange(layout)
+
+
+def _worker(rank, world, port, field_id, log_n, L, q, pieces=1):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from ntt_amd.distributed import FourStep, Layout
@@ -34,7 +42,9 @@ def _worker(rank, world, port, field_id, log_n, L, q):
         x = R.random_vector(field_id, n, seed=77)
         share = row_shares(x, Layout, log_n, world, L)[rank]
         eng = CpuOracleEngine(field_id, log_n, L, world, rank)
-        fs = FourStep(Layout(log_n, world, rank), eng, lambda s, r: dist.all_to_all_single(r.view(-1), s.view(-1)))
+        lay = Layout(log_n, world, rank)
+        fs = FourStep(lay, eng, _exchange(lay, pieces), pieces=pieces)
+        assert len(fs.pieces) == min(pieces, lay.r)
         fs.forward(share)
         fwd = share.clone()
         fs.inverse(share)
@@ -46,15 +56,18 @@ def _worker(rank, world, port, field_id, log_n, L, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,field_id,log_n", [(2, 1, 6), (2, 2, 7), (4, 1, 8)])
-def test_four_step_gloo(world, field_id, log_n):
+@pytest.mark.parametrize("world,field_id,log_n,pieces", [(2, 1, 6, 1), (2, 2, 7, 1), (4, 1, 8, 1), (2, 1, 6, 2),
+                                                          (2, 2, 7, 3), (4, 1, 8, 4)])
+def test_four_step_gloo(world, field_id, log_n, pieces):
+    """pieces > 1: the pipelined schedule (row transforms and the all-to-all in row pieces, uneven
+    last piece included) gives the same column layout and round trip."""
     from ntt_amd.distributed import Layout
     from tests.dist_helpers import gather_cols
     L = 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, field_id, log_n, L, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, field_id, log_n, L, q, pieces)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -92,7 +105,7 @@ def test_layout_rejects_bad_world():
         Layout(4, 8, 0)
 
 
-def _polymul_worker(rank, world, port, field_id, log_n, L, square, q):
+def _polymul_worker(rank, world, port, field_id, log_n, L, square, q, pieces=1):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from ntt_amd.distributed import FourStep, Layout
@@ -108,15 +121,18 @@ def _polymul_worker(rank, world, port, field_id, log_n, L, square, q):
         sb = sa if square else row_shares(b, Layout, log_n, world, L)[rank]
         out = torch.zeros_like(sa)
         eng = CpuOracleEngine(field_id, log_n, L, world, rank)
-        fs = FourStep(Layout(log_n, world, rank), eng, lambda s, r: dist.all_to_all_single(r.view(-1), s.view(-1)))
+        lay = Layout(log_n, world, rank)
+        fs = FourStep(lay, eng, _exchange(lay, pieces), pieces=pieces)
         fs.polymul(sa, sb, out)
         q.put((rank, out.numpy().tobytes()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,field_id,log_n,square", [(2, 1, 6, False), (4, 1, 8, False), (2, 2, 7, True)])
-def test_distributed_polymul_gloo(world, field_id, log_n, square):
+@pytest.mark.parametrize("world,field_id,log_n,square,pieces", [(2, 1, 6, False, 1), (4, 1, 8, False, 1),
+                                                                 (2, 2, 7, True, 1), (2, 1, 6, False, 2),
+                                                                 (4, 1, 8, False, 4), (2, 2, 7, True, 2)])
+def test_distributed_polymul_gloo(world, field_id, log_n, square, pieces):
     """C5's schedule (forward(a), forward(b) in ONE all-to-all, local pointwise product fused into
     the inverse, inverse all-to-all) over gloo: the row-layout result equals the oracle's cyclic
     product; squaring (a is b) takes the single-vector exchange."""
@@ -126,7 +142,7 @@ def test_distributed_polymul_gloo(world, field_id, log_n, square):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_polymul_worker, args=(r, world, port, field_id, log_n, L, square, q))
+    procs = [ctx.Process(target=_polymul_worker, args=(r, world, port, field_id, log_n, L, square, q, pieces))
              for r in range(world)]
     for p in procs:
         p.start()

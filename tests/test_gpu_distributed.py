@@ -23,9 +23,13 @@ def _index(layout, kind):
     return layout.rank * layout.c + kc + layout.n2 * k1
 
 
-@pytest.mark.parametrize("world,log_n,field_id,L", [(1, 12, 1, 4), (2, 12, 1, 4), (4, 16, 1, 4), (8, 20, 1, 4),
-                                                     (8, 16, 2, 6), (2, 14, 0, 1)])
-def test_virtual_ranks_match_single_gpu(world, log_n, field_id, L):
+@pytest.mark.parametrize("world,log_n,field_id,L,pieces", [(1, 12, 1, 4, 1), (2, 12, 1, 4, 1), (4, 16, 1, 4, 1),
+                                                            (8, 20, 1, 4, 1), (8, 16, 2, 6, 1), (2, 14, 0, 1, 1),
+                                                            (2, 12, 1, 4, 4), (8, 20, 1, 4, 4), (4, 16, 1, 4, 3),
+                                                            (8, 16, 2, 6, 2), (2, 14, 0, 1, 8)])
+def test_virtual_ranks_match_single_gpu(world, log_n, field_id, L, pieces):
+    """pieces > 1: the pipelined schedule (row pieces exchanged on a side stream while the next
+    piece is transformed) -- same column layout, same round trip."""
     from ntt_amd.distributed import VirtualRanks
     from ntt_amd.ntt import NTTPlan
     ref = NTTPlan(field_id, log_n, L)
@@ -33,7 +37,7 @@ def test_virtual_ranks_match_single_gpu(world, log_n, field_id, L):
     ref.fill(x, "random", seed=42)
     x0 = x.clone()
     ref.forward(x)
-    vr = VirtualRanks(field_id, log_n, L, world)
+    vr = VirtualRanks(field_id, log_n, L, world, pieces=pieces)
     xs = vr.fill(vr.empty(), "random", seed=42)
     for fs, t in zip(vr.ranks, xs):  # row-layout shares hold the right global elements
         assert torch.equal(t, x0[_index(fs.L, "row")])

@@ -61,14 +61,15 @@ def _single_gpu_product(fid, L, log_n, seed_a, seed_b):
     return c
 
 
-@pytest.mark.parametrize("world,fid,L,log_n,square", [(1, 1, 4, 12, False), (2, 1, 4, 13, False),
-                                                      (4, 1, 4, 16, False), (8, 1, 4, 20, False),
-                                                      (8, 2, 6, 16, False), (2, 0, 1, 14, False),
-                                                      (4, 1, 4, 14, True)])
-def test_virtual_ranks_polymul_matches_single_gpu(world, fid, L, log_n, square):
+@pytest.mark.parametrize("world,fid,L,log_n,square,pieces", [(1, 1, 4, 12, False, 1), (2, 1, 4, 13, False, 1),
+                                                             (4, 1, 4, 16, False, 1), (8, 1, 4, 20, False, 1),
+                                                             (8, 2, 6, 16, False, 1), (2, 0, 1, 14, False, 1),
+                                                             (4, 1, 4, 14, True, 1), (4, 1, 4, 16, False, 4),
+                                                             (8, 2, 6, 16, False, 3), (4, 1, 4, 14, True, 2)])
+def test_virtual_ranks_polymul_matches_single_gpu(world, fid, L, log_n, square, pieces):
     from ntt_amd.distributed import VirtualRanks
     exp = _single_gpu_product(fid, L, log_n, 5, None if square else 6)
-    vr = VirtualRanks(fid, log_n, L, world)
+    vr = VirtualRanks(fid, log_n, L, world, pieces=pieces)
     As = vr.fill(vr.empty(), "random", seed=5)
     Bs = As if square else vr.fill(vr.empty(), "random", seed=6)
     Outs = vr.empty()
@@ -82,7 +83,7 @@ def test_c5_polymul_2pow24_eight_virtual_ranks():
     from ntt_amd.distributed import VirtualRanks
     fid, L, log_n, world = 1, 4, 24, 8
     exp = _single_gpu_product(fid, L, log_n, 5, 6)
-    vr = VirtualRanks(fid, log_n, L, world)
+    vr = VirtualRanks(fid, log_n, L, world, pieces=4)  # the pipelined exchange, as timed in bench_configs
     As = vr.fill(vr.empty(), "random", seed=5)
     Bs = vr.fill(vr.empty(), "random", seed=6)
     vr.polymul(As, Bs, As)  # out aliases a

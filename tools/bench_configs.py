@@ -85,13 +85,15 @@ def main():
          passes=pl.passes)
     del pl, t
     torch.cuda.empty_cache()
-    vr = VirtualRanks(1, 28, 4, 8)
-    xs = vr.fill(vr.empty(), "random", seed=4)
-    emit("C4: 2^28 forward BN254 Fr, four-step over 8 virtual ranks on one GPU", 1 << 28,
-         timeit(lambda: vr.forward(xs), 2, 3),
-         note="exchange = device copies on one GPU; the RCCL all-to-all is timed by bench.py --four-step")
-    del vr, xs
-    torch.cuda.empty_cache()
+    for pieces in (1, 4):
+        vr = VirtualRanks(1, 28, 4, 8, pieces=pieces)
+        xs = vr.fill(vr.empty(), "random", seed=4)
+        emit(f"C4: 2^28 forward BN254 Fr, four-step over 8 virtual ranks on one GPU, {pieces} exchange piece(s)",
+             1 << 28, timeit(lambda: vr.forward(xs), 2, 3), pieces=pieces,
+             note="exchange = device copies on one GPU (side stream, overlapping the row transforms when "
+                  "pieces > 1); the RCCL all-to-all is timed by bench.py --four-step")
+        del vr, xs
+        torch.cuda.empty_cache()
 
     # C5 and coset
     pl = NTTPlan(1, 24, 4)
@@ -115,13 +117,16 @@ def main():
     emit("coset forward 2^24 BN254 Fr (shift = generator 5)", 1 << 24, timeit(lambda: pl.forward_coset(a, 5)))
     del pl, a, b, c
     torch.cuda.empty_cache()
-    vr = VirtualRanks(1, 24, 4, 8)
-    As = vr.fill(vr.empty(), "random", seed=5)
-    Bs = vr.fill(vr.empty(), "random", seed=6)
-    Cs = vr.empty()
-    emit("C5: polymul length 2^24 BN254 Fr, distributed schedule over 8 virtual ranks on one GPU", 1 << 24,
-         timeit(lambda: vr.polymul(As, Bs, Cs), 5, 10),
-         note="2 exchanges (a and b batched in one) as device copies; RCCL timing needs a multi-GPU node")
+    for pieces in (1, 4):
+        vr = VirtualRanks(1, 24, 4, 8, pieces=pieces)
+        As = vr.fill(vr.empty(), "random", seed=5)
+        Bs = vr.fill(vr.empty(), "random", seed=6)
+        Cs = vr.empty()
+        emit(f"C5: polymul length 2^24 BN254 Fr, distributed schedule over 8 virtual ranks on one GPU, "
+             f"{pieces} exchange piece(s)", 1 << 24, timeit(lambda: vr.polymul(As, Bs, Cs), 5, 10), pieces=pieces,
+             note="2 exchanges (a and b batched in one) as device copies; RCCL timing needs a multi-GPU node")
+        del vr, As, Bs, Cs
+        torch.cuda.empty_cache()
 
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     with open(args.out, "w") as f:
