@@ -80,8 +80,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--four-step", "--dist", dest="four_step", action="store_true",
                     help="one transform split over all ranks (four-step + RCCL all-to-all); default for N > 1")
-    ap.add_argument("--pieces", type=int, default=4,
-                    help="four-step: row pieces whose all-to-all overlaps the next piece's row transforms")
+    ap.add_argument("--pieces", type=int, default=None,
+                    help="four-step: row pieces whose all-to-all overlaps the next piece's row transforms "
+                         "(default: DistNTT.auto_pieces, >= 2^22 elements per piece)")
     ap.add_argument("--independent", action="store_true",
                     help="N > 1: one independent transform per rank (weak scaling, no data-path collective)")
     ap.add_argument("--cpu-log-n", type=int, default=22, help="C-oracle single-core sample size (log2)")

@@ -255,10 +255,25 @@ class DistNTT:
     (FourStep).
     """
 
+    # A piece's row transforms must still fill the GPU: every pass of a local transform launches one
+    # 1024-element workgroup tile per 1024 elements, and 256 CUs x 4 resident workgroups want several
+    # rounds of them.  Measured on one GPU (profiles/r02_pipe/, configs.jsonl): 2^28 over 8 virtual
+    # ranks (2^25 per rank) 34.5 -> 33.5 ms with 4 pieces; 2^24 polymul over 8 (2^21 per rank)
+    # 6.8 -> 8.0 ms with 4 pieces (half-empty launches).
+    MIN_PIECE_ELEMS = 1 << 22
+
+    @classmethod
+    def auto_pieces(cls, local_n: int, cap: int = 8) -> int:
+        k = 1
+        while k < cap and local_n // (2 * k) >= cls.MIN_PIECE_ELEMS:
+            k *= 2
+        return k
+
     def __init__(self, field_id: int = 1, log_n: int = 24, limbs64: int = 4, device: Optional[int] = None,
-                 group=None, host_exchange: bool = False, pieces: int = 4):
+                 group=None, host_exchange: bool = False, pieces: Optional[int] = None):
         """host_exchange: stage the all-to-all through host memory over a gloo group (rehearsing
-        several ranks on ONE GPU, where RCCL refuses duplicate devices); never the product path."""
+        several ranks on ONE GPU, where RCCL refuses duplicate devices); never the product path.
+        pieces: row pieces of the pipelined exchange (None: auto_pieces of the local share)."""
         import torch.distributed as dist
         self.dist = dist
         self.group = group
@@ -271,6 +286,8 @@ class DistNTT:
         self.field_id, self.log_n, self.limbs64 = field_id, log_n, limbs64
         self.layout = Layout(log_n, world, rank)
         self.engine = RankPlan(field_id, log_n, limbs64, world, rank, device)
+        if pieces is None:
+            pieces = self.auto_pieces(self.layout.local_n)
         self.fs = FourStep(self.layout, self.engine, self, pieces=1 if world == 1 else pieces)
         self.n = self.layout.n
         self.passes: List[int] = []  # per-transform schedules: see the row / column plans

@@ -165,3 +165,21 @@ def test_distributed_polymul_gloo(world, field_id, log_n, square, pieces):
         for i, v in enumerate(vals):
             got[lay.row_global(i)] = v
     assert got == exp
+
+
+def test_piece_ranges_and_auto_pieces():
+    """Row pieces tile [0, r) exactly (uneven last piece allowed); the automatic count keeps every
+    piece's row transforms >= 2^22 elements (full GPU launches) and never exceeds the cap."""
+    from ntt_amd.distributed import DistNTT, FourStep
+    for r in (1, 2, 3, 4, 7, 512, 2048):
+        for k in (1, 2, 3, 4, 8, 100):
+            pr = FourStep.piece_ranges(r, k)
+            assert len(pr) <= min(k, r)
+            assert pr[0][0] == 0 and all(a + n == b for (a, n), (b, _) in zip(pr, pr[1:]))
+            assert pr[-1][0] + pr[-1][1] == r and all(n >= 1 for _, n in pr)
+    assert DistNTT.auto_pieces(1 << 21) == 1  # 2^24 over 8 GPUs: one piece
+    assert DistNTT.auto_pieces(1 << 25) == 8  # C4: 2^28 over 8 GPUs
+    assert DistNTT.auto_pieces(1 << 23) == 2
+    for ln in range(10, 32):
+        k = DistNTT.auto_pieces(1 << ln)
+        assert k == 1 or (1 << ln) // k >= DistNTT.MIN_PIECE_ELEMS
