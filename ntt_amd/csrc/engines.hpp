@@ -31,6 +31,9 @@
 #ifndef NTT_P_PASS1_TABLE
 #define NTT_P_PASS1_TABLE 0
 #endif
+#ifndef NTT_P_LDS_TW
+#define NTT_P_LDS_TW 1
+#endif
 #ifndef NTT_TILE_LOG_P
 #define NTT_TILE_LOG_P 13
 #endif
@@ -78,6 +81,9 @@ struct Eng29 {
   // column passes after the first take their outer twiddles as Shoup pairs (w, ws) from L2-resident
   // tables (E::TW words per entry): 143 MADs per product instead of the Montgomery product's 162
   static constexpr bool SHOUP_OUTER = (L == 9);
+  // no LDS twiddle staging: a radix-256 table of Shoup pairs (20 KiB) beside the 36-KiB tile would
+  // halve the workgroups per CU
+  static constexpr bool LDS_TW = false;
   // quotient-estimate reduction needs p's top limb >= 2^18: possible only when 29L - 18 <= 255
   static constexpr bool FASTRED = 29 * L - 18 <= 255;
   struct Tw {
@@ -304,6 +310,10 @@ struct Eng32 {
   // products) instead of streaming an n-entry table (+50 % pass-1 traffic)
   static constexpr bool PASS1_FULL_TABLE = (N == 1) ? NTT_P_PASS1_TABLE : true;
   static constexpr bool SHOUP_OUTER = false;
+  // the parallel-load stage (parallel-load.cu:114-193, re-derived): the pass's w_R^e table (R <= 512
+  // words) is staged into LDS while the tile's HBM loads are in flight; sub-stages read twiddles
+  // from LDS instead of issuing L1/L2 loads beside the data stream
+  static constexpr bool LDS_TW = (N == 1) && NTT_P_LDS_TW;
   static constexpr int WAVES_PER_EU = 4;
   static constexpr bool LDS_SPLIT = false;
   struct Tw {

@@ -157,6 +157,14 @@ __device__ __forceinline__ void twiddle_mul(uint32_t (&x)[E::W], const uint32_t*
   E::tload(w, tab, e);
   E::mul(x, w, F);
 }
+// the same from the LDS copy of the table (E::LDS_TW engines: one word per entry)
+template <class E>
+__device__ __forceinline__ void twiddle_mul_lds(uint32_t (&x)[E::W], const uint32_t* lds_tw, uint32_t e,
+                                                const typename E::Args& F) {
+  typename E::Tw w;
+  w.w[0] = lds_tw[e];
+  E::mul(x, w, F);
+}
 
 // LDS slot of (local column/block c, in-column position pi): column-minor like HBM, with c XOR-ed
 // by the low bits of pi so that both lane orders used (c fastest, or pi fastest) hit distinct
@@ -208,9 +216,10 @@ __device__ __forceinline__ void sub_map(uint32_t t, int j, uint32_t rot, uint32_
 }
 
 // One LDS exchange + in-register radix-Q sub-stage s (s >= 1).
-template <class E, int LOGR, int T, int TE, int NT, int s, bool FAST, bool R32>
+template <class E, int LOGR, int T, int TE, int NT, int s, bool FAST, bool R32, bool LTW>
 __device__ __forceinline__ void substage(uint32_t (&x)[E::EPT][E::W], uint32_t (&cl)[E::EPT / 2],
-                                         uint32_t (&pil)[E::EPT / 2], uint32_t* lds, const PassArgs<E>& A, int t) {
+                                         uint32_t (&pil)[E::EPT / 2], uint32_t* lds, const PassArgs<E>& A, int t,
+                                         const uint32_t* lds_tw) {
   using S = Sched<LOGR, ept_log<E>()>;
   constexpr int EPT = E::EPT;
   constexpr int pqb = S::qb(s - 1), PQ = 1 << pqb, PG = EPT / PQ, psb = S::logsig(s - 1), plN = S::logN(s - 1);
@@ -258,7 +267,10 @@ __device__ __forceinline__ void substage(uint32_t (&x)[E::EPT][E::W], uint32_t (
       auto twiddles = [&]() {
         static_for<Q - 1>([&](auto K1) {
           constexpr int k = K1 + 1;
-          twiddle_mul<E>(x[j * Q + brev_bits(k, qb)], A.tw_int, (cp * k) << (LOGR - lN), A.F);
+          if constexpr (LTW)
+            twiddle_mul_lds<E>(x[j * Q + brev_bits(k, qb)], lds_tw, (cp * k) << (LOGR - lN), A.F);
+          else
+            twiddle_mul<E>(x[j * Q + brev_bits(k, qb)], A.tw_int, (cp * k) << (LOGR - lN), A.F);
         });
       };
       if constexpr (Uniform<LOGR, ept_log<E>(), NT, s>::on) {
@@ -301,6 +313,10 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
   constexpr int NT = TE / EPT;   // threads
   static_assert(LOGR >= QB && T >= 1, "radix");
   __shared__ __attribute__((aligned(16))) uint32_t lds[TE * LdsParts<E::LDSW, E::LDS_SPLIT>::max_words()];
+  // E::LDS_TW (parallel-load stage): this pass's w_R^e table in LDS -- not in a first pass with
+  // two-level outer twiddles (the P path's pass 1), where it measured slower (profiles/r02_ldstw/)
+  constexpr bool LTW = E::LDS_TW && !(KIND == KIND_COLUMN && !FULLTW);
+  __shared__ uint32_t lds_tw[LTW ? (1 << LOGR) : 1];
 
   // HBM words per element: the caller's buffers hold E::MEMW, the plan's scratch and outer-twiddle
   // tables E::SCRW (8 for 256-bit values in the 48-B layout).  Column passes read the caller's
@@ -384,6 +400,15 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
   uint32_t pil[EPT / 2];  // group index of each group
 
   // ------------------------------------------------------------------ sub-stage 0: global -> regs
+  // E::LDS_TW: this pass's w_R^e words, loaded ahead of the tile (L2 hits) and stored to LDS after
+  // sub-stage 0 (which still multiplies from the global table)
+  uint32_t stw[LTW ? ((1 << LOGR) + NT - 1) / NT : 1];
+  if constexpr (LTW && S::nsub > 1) {
+    static_for<((1 << LOGR) + NT - 1) / NT>([&](auto I) {
+      constexpr int i = I;
+      stw[i] = (t + NT * i < (1 << LOGR)) ? A.tw_int[t + NT * i] : 0u;
+    });
+  }
   {
     constexpr int qb = S::qb(0), Q = 1 << qb, G = EPT / Q, sb = S::logsig(0);
     static_for<G>([&](auto J) {
@@ -448,14 +473,22 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
         });
       }
     });
+    if constexpr (LTW && S::nsub > 1) {
+      // parallel-load stage: the table words loaded with the tile (above) go to LDS now; the first
+      // exchange's barrier publishes them to sub-stages 1.. (no barrier of its own)
+      static_for<((1 << LOGR) + NT - 1) / NT>([&](auto I) {
+        constexpr int i = I;
+        if (t + NT * i < (1 << LOGR)) lds_tw[t + NT * i] = stw[i];
+      });
+    }
   }
 
   // ------------------------------------------------------------------ sub-stages 1..nsub-1 via LDS
-  if constexpr (S::nsub > 1) substage<E, LOGR, T, TE, NT, 1, FAST, R32>(x, cl, pil, lds, A, t);
-  if constexpr (S::nsub > 2) substage<E, LOGR, T, TE, NT, 2, FAST, R32>(x, cl, pil, lds, A, t);
-  if constexpr (S::nsub > 3) substage<E, LOGR, T, TE, NT, 3, FAST, R32>(x, cl, pil, lds, A, t);
-  if constexpr (S::nsub > 4) substage<E, LOGR, T, TE, NT, 4, FAST, R32>(x, cl, pil, lds, A, t);
-  if constexpr (S::nsub > 5) substage<E, LOGR, T, TE, NT, 5, FAST, R32>(x, cl, pil, lds, A, t);
+  if constexpr (S::nsub > 1) substage<E, LOGR, T, TE, NT, 1, FAST, R32, LTW>(x, cl, pil, lds, A, t, lds_tw);
+  if constexpr (S::nsub > 2) substage<E, LOGR, T, TE, NT, 2, FAST, R32, LTW>(x, cl, pil, lds, A, t, lds_tw);
+  if constexpr (S::nsub > 3) substage<E, LOGR, T, TE, NT, 3, FAST, R32, LTW>(x, cl, pil, lds, A, t, lds_tw);
+  if constexpr (S::nsub > 4) substage<E, LOGR, T, TE, NT, 4, FAST, R32, LTW>(x, cl, pil, lds, A, t, lds_tw);
+  if constexpr (S::nsub > 5) substage<E, LOGR, T, TE, NT, 5, FAST, R32, LTW>(x, cl, pil, lds, A, t, lds_tw);
   static_assert(S::nsub <= 6, "sub-stages");
 
   // ------------------------------------------------------------------ output
