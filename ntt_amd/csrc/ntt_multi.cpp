@@ -11,6 +11,12 @@
 // grouped over the devices) -> interleaved n1-point NTTs reading the chunks as they arrived.  The
 // inverse mirrors it (column layout in, row layout out).  All work is asynchronous on the callers'
 // per-device streams.  The reference has no multi-GPU code.
+//
+// Pipelined exchange (as DistNTT, ntt_amd/distributed.py): the row steps run in row pieces
+// (ntt_rplan_*_rows_range); rows [a0, a0 + m) of every peer chunk are one contiguous run, so piece i
+// is exchanged (grouped ncclSend / ncclRecv on a per-device communication stream, ordered by events)
+// while the row transforms of piece i + 1 run, and the inverse transforms piece i as soon as it has
+// arrived.  Pieces keep >= 2^22 elements each (full launches); ntt_mplan_set_pieces overrides.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -71,6 +77,10 @@ struct ntt_mplan {
   std::vector<void*> send, recv;    // [G][chunk] per device
   std::vector<void*> send2, recv2;  // [G][2][chunk]: the polymul's batched (a, b) exchange, on first use
   std::vector<ncclComm_t> comm;
+  std::vector<hipStream_t> cstream;   // per-device communication stream (pipelined exchange)
+  std::vector<hipEvent_t> ev_ready;   // per device: compute -> communication ordering
+  std::vector<hipEvent_t> ev_done;    // per device and piece: arrival of piece i (kMaxPieces each)
+  unsigned pieces = 1;
 
   ~ntt_mplan() {
     int cur = 0;
@@ -78,13 +88,19 @@ struct ntt_mplan {
     for (size_t g = 0; g < dev.size(); ++g) {
       (void)hipSetDevice(dev[g]);
       if (g < comm.size() && comm[g]) rccl().CommDestroy(comm[g]);
+      if (g < cstream.size() && cstream[g]) (void)hipStreamDestroy(cstream[g]);
+      if (g < ev_ready.size() && ev_ready[g]) (void)hipEventDestroy(ev_ready[g]);
+      for (size_t i = g * kMaxPieces; i < (g + 1) * kMaxPieces && i < ev_done.size(); ++i)
+        if (ev_done[i]) (void)hipEventDestroy(ev_done[i]);
       for (auto* v : {&send, &recv, &send2, &recv2})
         if (g < v->size() && (*v)[g]) (void)hipFree((*v)[g]);
       if (g < rp.size() && rp[g]) ntt_rplan_destroy(rp[g]);
     }
     (void)hipSetDevice(cur);
   }
+  static constexpr unsigned kMaxPieces = 16;
   size_t local_n() const { return 1ull << (log_n - log_g); }
+  hipEvent_t done(int g, unsigned i) const { return ev_done[g * kMaxPieces + i]; }
   hipStream_t stream(void* const* streams, int g) const {
     return streams ? static_cast<hipStream_t>(streams[g]) : nullptr;
   }
@@ -139,6 +155,67 @@ size_t chunk_words(const ntt_mplan* m) {  // per-peer chunk of one vector: r * c
   return (1ull << (m->log_r + m->log_c)) * (m->elem_bytes / 8);
 }
 
+// Rows [row0, row0 + nrows) of every peer chunk of nv vectors (buffers [G][nv][chunk]), as grouped
+// ncclSend / ncclRecv on the communication streams.
+int exchange_rows(ntt_mplan* m, const std::vector<void*>& send, const std::vector<void*>& recv, int nv,
+                  size_t row0, size_t nrows) {
+  const Rccl& R = rccl();
+  const size_t cw = chunk_words(m), rw = cw >> m->log_r;  // words per chunk, per chunk row
+  const size_t off0 = row0 * rw, words = nrows * rw, piece = kMaxPeerBytes / 8;
+  if (R.GroupStart() != ncclSuccess) return NTT_ERR_RCCL;
+  ncclResult_t st = ncclSuccess;
+  for (int g = 0; g < m->ngpus && st == ncclSuccess; ++g) {
+    hipSetDevice(m->dev[g]);
+    auto* sb = static_cast<uint64_t*>(send[g]);
+    auto* rb = static_cast<uint64_t*>(recv[g]);
+    for (int h = 0; h < m->ngpus && st == ncclSuccess; ++h)
+      for (int k = 0; k < nv && st == ncclSuccess; ++k) {
+        const size_t base = (size_t)(h * nv + k) * cw + off0;
+        for (size_t off = 0; off < words && st == ncclSuccess; off += piece) {
+          const size_t cnt = words - off < piece ? words - off : piece;
+          st = R.Send(sb + base + off, cnt, ncclUint64, h, m->comm[g], m->cstream[g]);
+          if (st == ncclSuccess) st = R.Recv(rb + base + off, cnt, ncclUint64, h, m->comm[g], m->cstream[g]);
+        }
+      }
+  }
+  const ncclResult_t end = R.GroupEnd();
+  return (st == ncclSuccess && end == ncclSuccess) ? NTT_OK : NTT_ERR_RCCL;
+}
+
+// comm stream of every device waits for the work enqueued so far on its compute stream
+int order_comm_after_compute(ntt_mplan* m, void* const* streams) {
+  for (int g = 0; g < m->ngpus; ++g) {
+    hipSetDevice(m->dev[g]);
+    if (hipEventRecord(m->ev_ready[g], m->stream(streams, g)) != hipSuccess ||
+        hipStreamWaitEvent(m->cstream[g], m->ev_ready[g], 0) != hipSuccess)
+      return NTT_ERR_HIP;
+  }
+  return NTT_OK;
+}
+
+// compute stream of every device waits for piece i's arrival (recorded on its comm stream)
+int order_compute_after_piece(ntt_mplan* m, void* const* streams, unsigned i) {
+  for (int g = 0; g < m->ngpus; ++g) {
+    hipSetDevice(m->dev[g]);
+    if (hipStreamWaitEvent(m->stream(streams, g), m->done(g, i), 0) != hipSuccess) return NTT_ERR_HIP;
+  }
+  return NTT_OK;
+}
+
+int record_piece(ntt_mplan* m, unsigned i) {
+  for (int g = 0; g < m->ngpus; ++g) {
+    hipSetDevice(m->dev[g]);
+    if (hipEventRecord(m->done(g, i), m->cstream[g]) != hipSuccess) return NTT_ERR_HIP;
+  }
+  return NTT_OK;
+}
+
+void piece_range(const ntt_mplan* m, unsigned i, size_t& row0, size_t& nrows) {
+  const size_t r = 1ull << m->log_r, step = (r + m->pieces - 1) / m->pieces;
+  row0 = i * step;
+  nrows = row0 >= r ? 0 : (r - row0 < step ? r - row0 : step);
+}
+
 // After a failed step the other devices may still hold queued work that reads or writes the
 // caller's buffers: wait for every device's stream before reporting the error, so the caller can
 // free or reuse them.
@@ -146,6 +223,7 @@ int drain(ntt_mplan* m, void* const* streams, int rc) {
   for (int g = 0; g < m->ngpus; ++g) {
     (void)hipSetDevice(m->dev[g]);
     (void)hipStreamSynchronize(m->stream(streams, g));
+    if (g < (int)m->cstream.size() && m->cstream[g]) (void)hipStreamSynchronize(m->cstream[g]);
   }
   return rc;
 }
@@ -177,11 +255,30 @@ int ensure_pair_buffers(ntt_mplan* m) {
 int forward_vectors(ntt_mplan* m, void* const* const* v, int nv, void* const* streams) {
   const std::vector<void*>& sb = nv == 1 ? m->send : m->send2;
   const std::vector<void*>& rb = nv == 1 ? m->recv : m->recv2;
-  for (int g = 0; g < m->ngpus; ++g)
-    for (int k = 0; k < nv; ++k)
-      if (int rc = ntt_rplan_forward_rows(m->rp[g], v[k][g], sb[g], (unsigned)nv, (unsigned)k, m->stream(streams, g)))
-        return rc;
-  if (int rc = exchange(m, sb, rb, nv * chunk_words(m), streams)) return rc;
+  if (m->pieces == 1) {
+    for (int g = 0; g < m->ngpus; ++g)
+      for (int k = 0; k < nv; ++k)
+        if (int rc = ntt_rplan_forward_rows(m->rp[g], v[k][g], sb[g], (unsigned)nv, (unsigned)k,
+                                            m->stream(streams, g)))
+          return rc;
+    if (int rc = exchange(m, sb, rb, nv * chunk_words(m), streams)) return rc;
+  } else {  // piece i's exchange overlaps the row transforms of piece i + 1
+    for (unsigned i = 0; i < m->pieces; ++i) {
+      size_t a0, ra;
+      piece_range(m, i, a0, ra);
+      if (ra == 0) break;
+      for (int g = 0; g < m->ngpus; ++g)
+        for (int k = 0; k < nv; ++k)
+          if (int rc = ntt_rplan_forward_rows_range(m->rp[g], v[k][g], sb[g], (unsigned)nv, (unsigned)k, a0, ra,
+                                                    m->stream(streams, g)))
+            return rc;
+      if (int rc = order_comm_after_compute(m, streams)) return rc;
+      if (int rc = exchange_rows(m, sb, rb, nv, a0, ra)) return rc;
+      if (int rc = record_piece(m, i)) return rc;
+    }
+    for (unsigned i = 0; i < m->pieces; ++i)
+      if (int rc = order_compute_after_piece(m, streams, i)) return rc;
+  }
   for (int g = 0; g < m->ngpus; ++g)
     for (int k = 0; k < nv; ++k)
       if (int rc = ntt_rplan_forward_cols(m->rp[g], rb[g], v[k][g], (unsigned)nv, (unsigned)k, m->stream(streams, g)))
@@ -195,9 +292,30 @@ int inverse_vector(ntt_mplan* m, void* const* a, void* const* b, void* const* ou
   for (int g = 0; g < m->ngpus; ++g)
     if (int rc = ntt_rplan_inverse_cols(m->rp[g], a[g], b ? b[g] : nullptr, m->send[g], m->stream(streams, g)))
       return rc;
-  if (int rc = exchange(m, m->send, m->recv, chunk_words(m), streams)) return rc;
-  for (int g = 0; g < m->ngpus; ++g)
-    if (int rc = ntt_rplan_inverse_rows(m->rp[g], m->recv[g], out[g], m->stream(streams, g))) return rc;
+  if (m->pieces == 1) {
+    if (int rc = exchange(m, m->send, m->recv, chunk_words(m), streams)) return rc;
+    for (int g = 0; g < m->ngpus; ++g)
+      if (int rc = ntt_rplan_inverse_rows(m->rp[g], m->recv[g], out[g], m->stream(streams, g))) return rc;
+    return NTT_OK;
+  }
+  // every piece's exchange is queued on the comm streams; piece i's row transforms wait only for it
+  if (int rc = order_comm_after_compute(m, streams)) return rc;
+  for (unsigned i = 0; i < m->pieces; ++i) {
+    size_t a0, ra;
+    piece_range(m, i, a0, ra);
+    if (ra == 0) break;
+    if (int rc = exchange_rows(m, m->send, m->recv, 1, a0, ra)) return rc;
+    if (int rc = record_piece(m, i)) return rc;
+  }
+  for (unsigned i = 0; i < m->pieces; ++i) {
+    size_t a0, ra;
+    piece_range(m, i, a0, ra);
+    if (ra == 0) break;
+    if (int rc = order_compute_after_piece(m, streams, i)) return rc;
+    for (int g = 0; g < m->ngpus; ++g)
+      if (int rc = ntt_rplan_inverse_rows_range(m->rp[g], m->recv[g], out[g], a0, ra, m->stream(streams, g)))
+        return rc;
+  }
   return NTT_OK;
 }
 
@@ -236,6 +354,24 @@ int ntt_mplan_create(ntt_mplan** out, int field_id, unsigned log_n, unsigned lim
   if (rc == NTT_OK) {
     m->comm.assign(ngpus, nullptr);
     if (!rccl().ok() || rccl().CommInitAll(m->comm.data(), ngpus, devices) != ncclSuccess) rc = NTT_ERR_RCCL;
+  }
+  if (rc == NTT_OK) {
+    m->cstream.assign(ngpus, nullptr);
+    m->ev_ready.assign(ngpus, nullptr);
+    m->ev_done.assign((size_t)ngpus * ntt_mplan::kMaxPieces, nullptr);
+    for (int g = 0; g < ngpus && rc == NTT_OK; ++g) {
+      (void)hipSetDevice(devices[g]);
+      if (hipStreamCreateWithFlags(&m->cstream[g], hipStreamNonBlocking) != hipSuccess ||
+          hipEventCreateWithFlags(&m->ev_ready[g], hipEventDisableTiming) != hipSuccess)
+        rc = NTT_ERR_HIP;
+      for (unsigned i = 0; i < ntt_mplan::kMaxPieces && rc == NTT_OK; ++i)
+        if (hipEventCreateWithFlags(&m->ev_done[g * ntt_mplan::kMaxPieces + i], hipEventDisableTiming) != hipSuccess)
+          rc = NTT_ERR_HIP;
+    }
+    // pieces of >= 2^22 elements (DistNTT.auto_pieces)
+    const size_t local = m->local_n();
+    while (m->pieces < 8 && (local >> 1) / m->pieces >= (size_t(1) << 22)) m->pieces *= 2;
+    if (m->pieces > (1u << m->log_r)) m->pieces = 1u << m->log_r;
   }
   if (rc != NTT_OK) {
     delete m;
@@ -279,6 +415,12 @@ int ntt_mplan_fill(ntt_mplan* m, void* const* d_data, int kind, uint64_t seed, v
     (void)hipSetDevice(m->dev[g]);
     if (int rc = ntt_rplan_fill(m->rp[g], d_data[g], kind, seed, m->stream(streams, g))) return rc;
   }
+  return NTT_OK;
+}
+
+int ntt_mplan_set_pieces(ntt_mplan* m, unsigned pieces) {
+  if (!m || pieces < 1 || pieces > ntt_mplan::kMaxPieces || pieces > (1u << m->log_r)) return NTT_ERR_ARG;
+  m->pieces = pieces;
   return NTT_OK;
 }
 

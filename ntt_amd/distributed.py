@@ -446,7 +446,9 @@ class MultiPlan:
     being one grouped RCCL all-to-all.  Shares are torch tensors, ``xs[g]`` on ``devices[g]``.
     """
 
-    def __init__(self, field_id: int = 1, log_n: int = 24, limbs64: int = 4, devices: Optional[List[int]] = None):
+    def __init__(self, field_id: int = 1, log_n: int = 24, limbs64: int = 4, devices: Optional[List[int]] = None,
+                 pieces: Optional[int] = None):
+        """pieces: row pieces of the pipelined exchange (None: the plan's default, >= 2^22 elements each)."""
         from . import lib as _L
         self._L = _L
         self.lib = _L.load()
@@ -461,6 +463,8 @@ class MultiPlan:
         self.lib.ntt_mplan_info(h, C.byref(local_n), C.byref(n1), C.byref(n2))
         self.local_n, self.log_n1, self.log_n2 = local_n.value, n1.value, n2.value
         self.layouts = [Layout(log_n, len(self.devices), g) for g in range(len(self.devices))]
+        if pieces is not None:
+            _L.check(self.lib.ntt_mplan_set_pieces(h, int(pieces)), "ntt_mplan_set_pieces")
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -91,12 +91,12 @@ def test_c5_polymul_2pow24_eight_virtual_ranks():
         assert torch.equal(o, exp[_row_index(fs.L, o.device)]), fs.L.rank
 
 
-@pytest.mark.parametrize("log_n", [16, 24])
-def test_mplan_polymul_matches_single_gpu(log_n):
+@pytest.mark.parametrize("log_n,pieces", [(16, None), (24, None), (16, 4), (24, 8)])
+def test_mplan_polymul_matches_single_gpu(log_n, pieces):
     from ntt_amd.distributed import MultiPlan
     fid, L = 1, 4
     exp = _single_gpu_product(fid, L, log_n, 5, 6)
-    mp = MultiPlan(fid, log_n, L, devices=list(range(torch.cuda.device_count())))
+    mp = MultiPlan(fid, log_n, L, devices=list(range(torch.cuda.device_count())), pieces=pieces)
     As = mp.fill(mp.empty(), "random", seed=5)
     Bs = mp.fill(mp.empty(), "random", seed=6)
     Outs = mp.empty()
