@@ -72,6 +72,15 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
  * four-step DIF schedule; kept to measure against it (tools/bench_rivals.py).  P469762049 (1 limb)
  * and 4-limb plans, single transforms (batch 1); other calls use the default schedule. */
 #define NTT_PLAN_STOCKHAM 4u
+/* Rival schedule: forward transforms run as the reference's GZKP(B, G) (GZKP-NTT.cu:
+ * 115-165, driver 167-233; parallel-load.cu:114-193 for P): a bit-reversal permutation pass
+ * (`rearrange`), then in-place radix-2 DIT rounds, B of them per pass over tiles of G adjacent
+ * columns, re-derived as: the permutation into a plan buffer, a first pass of contiguous radix-2^r_0
+ * DFTs, then passes that multiply their inputs by w_N^(c d) (per-pass tables) and run radix-2^r_i
+ * DFTs in place over stride-2^(r_0 + .. + r_{i-1}) columns.  Same contract and results as the
+ * default schedule; P469762049 (1 limb) and 4-limb plans, single transforms (batch 1).
+ * NTT_PLAN_STOCKHAM and NTT_PLAN_GZKP are exclusive. */
+#define NTT_PLAN_GZKP 8u
 int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags);
 
 /* Modulus-generic plan, like big-num.cu's `prime` / `omega` kernel arguments (big-num.cu:68,173,260):

@@ -1,0 +1,5 @@
+// Eng256: k_pass instantiations for KIND_DIT (the reference's GZKP(B, G) rival schedule).
+#include "ntt_kernels_impl.hpp"
+namespace ntt {
+NTT_INSTANTIATE_KIND(Eng256, KIND_DIT)
+}  // namespace ntt

@@ -9,7 +9,9 @@ namespace ntt {
 // KIND_STOCKHAM: the rival schedule of the reference's bellperson / improved_NTT_v1..v4 family
 // (GZKP-NTT.cu:324-386, 556-1296): Stockham autosort passes, input-side twiddles, no final
 // permutation (ntt_plan_create_ex flag NTT_PLAN_STOCKHAM).
-enum : int { KIND_COLUMN = 0, KIND_FINAL = 1, KIND_SINGLE = 2, KIND_STOCKHAM = 3 };
+// KIND_DIT: the GZKP(B, G) rival (GZKP-NTT.cu:115-165): in-place DIT column passes with input-side
+// twiddles w_N^(c d) over bit-reversed data (ntt_plan_create_ex flag NTT_PLAN_GZKP).
+enum : int { KIND_COLUMN = 0, KIND_FINAL = 1, KIND_SINGLE = 2, KIND_STOCKHAM = 3, KIND_DIT = 4 };
 // engines with KIND_STOCKHAM instances (ntt_e256_stk.hip, ntt_ep_stk.hip)
 template <class E>
 struct HasStockham {
@@ -97,6 +99,11 @@ template <class E>
 hipError_t launch_build_tw_sh(uint32_t* out, size_t count, uint32_t log_r, uint32_t log_t, uint32_t log_m,
                               const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits, const typename E::Args& F,
                               const uint32_t* pinvB, hipStream_t st);
+// dst[i] = src[digit reversal of i] over 2^log_n elements of E::MEMW words, digits of digits[q] bits
+// in pass order (the GZKP rival's `rearrange`; all 1 = the bit reversal)
+template <class E>
+hipError_t launch_bitrev(const uint32_t* src, uint32_t* dst, uint32_t log_n, const uint32_t* digits, uint32_t nd,
+                         hipStream_t st);
 template <class E>
 hipError_t launch_build_fs_tw(uint32_t* out, uint32_t log_rows, uint32_t log_cols, uint64_t row0, uint64_t col0,
                               uint32_t log_n, const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits,

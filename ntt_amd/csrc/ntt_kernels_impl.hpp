@@ -306,7 +306,7 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                               const PassArgs<E> A) {
   constexpr int QB = ept_log<E>(), EPT = E::EPT;
   using S = Sched<LOGR, QB>;
-  constexpr bool COLLIKE = KIND == KIND_COLUMN || KIND == KIND_STOCKHAM;  // column-group geometry
+  constexpr bool COLLIKE = KIND == KIND_COLUMN || KIND == KIND_STOCKHAM || KIND == KIND_DIT;  // column groups
   constexpr int TE = (KIND == KIND_SINGLE) ? (1 << LOGR) : (1 << tile_log_of<E>());
   constexpr int T = TE >> LOGR;  // columns (column pass) or blocks (final / single) per workgroup
   constexpr bool R32 = KIND != KIND_COLUMN;  // reduce_top form (engines.hpp): column passes are at the VGPR cap
@@ -443,9 +443,11 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
           pos = pi;
         }
         E::template load<SW>(x[j * Q + d], src, NTT_NOMEM(IN_USER ? in_pos(pos) : pos));
-        if constexpr (KIND == KIND_STOCKHAM && FULLTW) {
+        if constexpr ((KIND == KIND_STOCKHAM || KIND == KIND_DIT) && FULLTW) {
           // bellperson's input twiddle (GZKP-NTT.cu:348-354): element pi of group k = index mod p is
-          // multiplied by w_n^((n >> lgp >> deg) k pi), from a [k / T][pi][k mod T] table (p >= T)
+          // multiplied by w_n^((n >> lgp >> deg) k pi), from a [k / T][pi][k mod T] table (p >= T).
+          // KIND_DIT (GZKP(B, G), in place after the bit reversal): column c < s = 2^lgp of a block of
+          // N = s R, input d multiplied by w_N^(c d) -- the same table shape with k = c
           uint32_t tw[E::W];
           const uint32_t k0 = col0 & ((1u << A.lgp) - 1);
           E::template load<E::SCRW>(tw, A.tw_full, ((size_t)k0 << LOGR) + pi * T + c);
@@ -506,7 +508,11 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
         const uint32_t pi = (rho << lN) + cp + (k << sb);
         const uint32_t kn = natural_index<LOGR, QB>(pi);
         size_t pos;
-        if constexpr (KIND == KIND_STOCKHAM) {
+        if constexpr (KIND == KIND_DIT) {
+          // in place (GZKP-NTT.cu:157-158): output k of column c back to c + s k of its block
+          pos = colbase + c + ((size_t)kn << log_s);
+          E::template store<E::IN * Q, FAST, DW>(dst, NTT_NOMEM(pos), v, A.F);
+        } else if constexpr (KIND == KIND_STOCKHAM) {
           // autosort store (GZKP-NTT.cu:378-384): y[((index - k) << deg) + k + kn p], k = index mod p
           const uint32_t idx = col0 + c, kk = idx & ((1u << A.lgp) - 1);
           pos = ((size_t)(idx - kk) << LOGR) + kk + ((size_t)kn << A.lgp);
@@ -694,6 +700,52 @@ hipError_t launch_build_tw_sh(uint32_t* out, size_t count, uint32_t log_r, uint3
                        log_r, log_t, log_m, lo, hi, lo_bits, F, pinvB);
     return hipGetLastError();
   }
+}
+
+// GZKP rival's `rearrange` (GZKP-NTT.cu:167-233 via reverse pairs), out of place: dst[i] = src[drev(i)].
+// The reference's rounds are radix 2, so its permutation is the bit reversal; here every pass is a
+// natural-order radix-2^r_q DFT, so the permutation that gives natural-order output is the mixed-radix
+// digit reversal: digit q of i (r_q bits, from the low end, in pass order) becomes digit q of the
+// source index counted from the HIGH end.  (All r_q = 1 gives the bit reversal.)
+struct DigitRev {
+  uint32_t nd;
+  uint32_t r[8];
+};
+template <int MEMW>
+__global__ void k_digitrev(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t log_n,
+                           DigitRev D) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >> log_n) return;
+  size_t j = 0, rem = i;
+  uint32_t top = log_n;
+  for (uint32_t q = 0; q < D.nd; ++q) {
+    top -= D.r[q];
+    j |= (rem & ((1ull << D.r[q]) - 1)) << top;
+    rem >>= D.r[q];
+  }
+  if constexpr (MEMW % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < MEMW / 4; ++q)
+      reinterpret_cast<uint4*>(dst + i * MEMW)[q] = reinterpret_cast<const uint4*>(src + j * MEMW)[q];
+  } else {
+#pragma unroll
+    for (int q = 0; q < MEMW; ++q) dst[i * MEMW + q] = src[j * MEMW + q];
+  }
+}
+
+template <class E>
+hipError_t launch_bitrev(const uint32_t* src, uint32_t* dst, uint32_t log_n, const uint32_t* digits, uint32_t nd,
+                         hipStream_t st) {
+  DigitRev D{};
+  uint32_t sum = 0;
+  if (nd > 8) return hipErrorInvalidValue;
+  D.nd = nd;
+  for (uint32_t q = 0; q < nd; ++q) sum += (D.r[q] = digits[q]);
+  if (sum != log_n) return hipErrorInvalidValue;
+  const size_t n = 1ull << log_n;
+  hipLaunchKernelGGL((k_digitrev<E::MEMW>), dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, src, dst, log_n,
+                     D);
+  return hipGetLastError();
 }
 
 // Four-step twiddle table of one rank (ntt_rplan): entry (a, b) at a 2^log_cols + b holds
@@ -986,7 +1038,7 @@ static hipError_t launch_plain(const uint32_t* src, uint32_t* dst, const PassArg
 template <class E, int KIND, int LOGR, bool FULLTW, bool FAST>
 static hipError_t launch_fsm(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, dim3 g, dim3 b,
                              hipStream_t st) {
-  if constexpr (KIND == KIND_STOCKHAM) {
+  if constexpr (KIND == KIND_STOCKHAM || KIND == KIND_DIT) {
     if (A.fs || A.tw_epi) return hipErrorInvalidValue;
     return launch_plain<E, LOGR, KIND, FULLTW, FAST, 0>(src, dst, A, g, b, st);
   }
@@ -1002,7 +1054,7 @@ static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassAr
                                 uint32_t batch, hipStream_t st) {
   constexpr int TL = tile_log_of<E>();
   constexpr int MAXR = (KIND == KIND_SINGLE) ? TL : TL - E::MIN_COLS_LOG;
-  if constexpr (LOGR > MAXR || (KIND == KIND_STOCKHAM && !HasStockham<E>::value)) {
+  if constexpr (LOGR > MAXR || ((KIND == KIND_STOCKHAM || KIND == KIND_DIT) && !HasStockham<E>::value)) {
     return hipErrorInvalidValue;
   } else {
     constexpr int TE = (KIND == KIND_SINGLE) ? (1 << LOGR) : (1 << TL);
@@ -1010,7 +1062,7 @@ static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassAr
     const dim3 g(grid, batch), b(NT < 64 ? 64 : NT);
     if constexpr (E::FASTRED) {
       if (A.F.red_ok) {
-        if constexpr (KIND == KIND_STOCKHAM) {
+        if constexpr (KIND == KIND_STOCKHAM || KIND == KIND_DIT) {
           return A.tw_full ? launch_fsm<E, KIND, LOGR, true, true>(src, dst, A, g, b, st)
                            : launch_fsm<E, KIND, LOGR, false, true>(src, dst, A, g, b, st);
         }
@@ -1034,7 +1086,7 @@ static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassAr
       }
     }
     if (A.src2 || A.tw_in) return hipErrorInvalidValue;
-    if constexpr (KIND == KIND_COLUMN || KIND == KIND_STOCKHAM) {
+    if constexpr (KIND == KIND_COLUMN || KIND == KIND_STOCKHAM || KIND == KIND_DIT) {
       if (A.tw_full) return launch_fsm<E, KIND, LOGR, true, false>(src, dst, A, g, b, st);
     }
     return launch_fsm<E, KIND, LOGR, false, false>(src, dst, A, g, b, st);
@@ -1065,9 +1117,11 @@ hipError_t launch_pass(int kind, int logr, const uint32_t* src, uint32_t* dst, c
                        uint32_t batch, hipStream_t st) {
   if (kind == KIND_COLUMN) return launch_pass_kind<E, KIND_COLUMN>(logr, src, dst, A, grid, batch, st);
   if (kind == KIND_FINAL) return launch_pass_kind<E, KIND_FINAL>(logr, src, dst, A, grid, batch, st);
-  if (kind == KIND_STOCKHAM) {
-    if constexpr (HasStockham<E>::value)
+  if (kind == KIND_STOCKHAM || kind == KIND_DIT) {
+    if constexpr (HasStockham<E>::value) {
+      if (kind == KIND_DIT) return launch_pass_kind<E, KIND_DIT>(logr, src, dst, A, grid, batch, st);
       return launch_pass_kind<E, KIND_STOCKHAM>(logr, src, dst, A, grid, batch, st);
+    }
     return hipErrorInvalidValue;
   }
   return launch_pass_kind<E, KIND_SINGLE>(logr, src, dst, A, grid, batch, st);
@@ -1113,6 +1167,7 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
   NTT_EXTERN_KIND(E, KIND_FINAL)                                                                                   \
   NTT_EXTERN_KIND(E, KIND_SINGLE)                                                                                  \
   NTT_EXTERN_KIND(E, KIND_STOCKHAM)                                                                                \
+  NTT_EXTERN_KIND(E, KIND_DIT)                                                                                     \
   template hipError_t launch_pass<E>(int, int, const uint32_t*, uint32_t*, const PassArgs<E>&, uint32_t, uint32_t, \
                                      hipStream_t);                                                                 \
   template hipError_t launch_naive<E>(const uint32_t*, uint32_t*, const PassArgs<E>&, uint32_t, hipStream_t);       \
@@ -1128,6 +1183,8 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
   template hipError_t launch_build_tw<E>(uint32_t*, size_t, uint32_t, uint32_t, uint32_t, const uint32_t*,        \
                                          const uint32_t*, uint32_t, const typename E::Args&, hipStream_t,          \
                                          const uint32_t*, const uint32_t*);                                        \
+  template hipError_t launch_bitrev<E>(const uint32_t*, uint32_t*, uint32_t, const uint32_t*, uint32_t,           \
+                                       hipStream_t);                                                              \
   template hipError_t launch_build_tw_sh<E>(uint32_t*, size_t, uint32_t, uint32_t, uint32_t, const uint32_t*,     \
                                             const uint32_t*, uint32_t, const typename E::Args&, const uint32_t*,  \
                                             hipStream_t);                                                         \

@@ -499,7 +499,9 @@ struct PlanImpl final : PlanBase {
       rc = NTT_ERR_HIP;
     if (rc == NTT_OK && npass >= 2 && !twiddle_only) rc = ensure_scratch(1);
     if (rc == NTT_OK && npass >= 2 && !twiddle_only) rc = build_full_tables();
-    if (rc == NTT_OK && (flags & NTT_PLAN_STOCKHAM)) rc = build_stockham();
+    // NTT_PLAN_GZKP runs on the same per-pass tables: Stockham pass i's w_n^((k pi) << (log_n - lgp_i - r_i))
+    // for k < 2^lgp_i is the GZKP DIT pass's w_N^(c d), N = 2^(lgp_i + r_i)
+    if (rc == NTT_OK && (flags & (NTT_PLAN_STOCKHAM | NTT_PLAN_GZKP))) rc = build_stockham();
     hipSetDevice(cur);
     return rc;
   }
@@ -539,6 +541,49 @@ struct PlanImpl final : PlanBase {
         lgp += ri;
       }
       return hipDeviceSynchronize() == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+    }
+  }
+
+  // NTT_PLAN_GZKP (rival schedule, GZKP(B, G), GZKP-NTT.cu:115-233): digit reversal into a plan buffer
+  // (`rearrange`; the bit reversal of the reference's radix-2 rounds), contiguous radix-2^r_0 DFTs (the reference's first rounds, `naive` / a GZKP launch
+  // at stride 1), then in-place DIT passes over stride-2^lgp columns with input twiddles; the last
+  // pass writes the caller's buffer.  Widest radix first, as for Stockham (lgp_i >= T_i).
+  int run_gzkp(const uint32_t* in, uint32_t* out, hipStream_t st) {
+    if constexpr (!HasStockham<E>::value) {
+      return NTT_ERR_ARG;
+    } else {
+      const unsigned tl = tile_log_of<E>();
+      uint32_t* buf = d_stk_buf[0];
+      uint32_t digits[8];
+      for (unsigned i = 0; i < npass; ++i) digits[i] = r[stk_ord[i]];
+      begin(st);
+      hipError_t e = launch_bitrev<E>(in, buf, log_n, digits, npass, st);
+      mark(st);
+      unsigned lgp = 0;
+      for (unsigned i = 0; i < npass && e == hipSuccess; ++i) {
+        const unsigned ri = r[stk_ord[i]];
+        PassArgs<E> A = base_args(false);
+        A.tw_int = d_tab + off_int_f[stk_ord[i]];  // w_R^e for this pass's radix
+        uint32_t* dst = i + 1 == npass ? out : buf;
+        if (i == 0) {  // s = 1: contiguous 2^r_0-point DFTs, batched (grid.y chunks of <= 2^15 blocks)
+          A.batch_stride = ((size_t)1 << ri) * MEMW;
+          const size_t blocks = n >> ri, chunk = size_t(1) << 15;
+          for (size_t b0 = 0; b0 < blocks && e == hipSuccess; b0 += chunk) {
+            const size_t off = (b0 << ri) * MEMW;
+            e = launch_pass<E>(KIND_SINGLE, (int)ri, buf + off, buf + off, A, 1,
+                               (uint32_t)(blocks - b0 < chunk ? blocks - b0 : chunk), st);
+          }
+        } else {
+          A.tw_full = d_stk_tab + stk_off[i] * SCRW;  // w_N^(c d), N = 2^(lgp + r_i)
+          A.log_blk = lgp + ri;
+          A.lgp = lgp;
+          A.src_user = 1;
+          e = launch_pass<E>(KIND_DIT, (int)ri, buf, dst, A, (uint32_t)(n >> tl), 1, st);
+        }
+        mark(st);
+        lgp += ri;
+      }
+      return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
     }
   }
 
@@ -799,6 +844,8 @@ struct PlanImpl final : PlanBase {
     if (!d || batch == 0 || (flags & NTT_PLAN_TWIDDLE_ONLY)) return NTT_ERR_ARG;
     if ((flags & NTT_PLAN_STOCKHAM) && !inverse && batch == 1 && d_stk_tab)
       return run_stockham(static_cast<uint32_t*>(d), static_cast<uint32_t*>(d), st);
+    if ((flags & NTT_PLAN_GZKP) && !inverse && batch == 1 && d_stk_tab)
+      return run_gzkp(static_cast<uint32_t*>(d), static_cast<uint32_t*>(d), st);
     return run_io(static_cast<uint32_t*>(d), nullptr, static_cast<uint32_t*>(d), batch, inverse, st);
   }
 
@@ -1030,6 +1077,7 @@ static int make_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, const 
                      unsigned log_n, int device, unsigned flags) {
   if (log_n > 40) return NTT_ERR_ARG;
   if (limbs64 != 1 && limbs64 != 4 && limbs64 != 6) return NTT_ERR_ARG;  // before packing into p32[12] / g32[12]
+  if ((flags & NTT_PLAN_STOCKHAM) && (flags & NTT_PLAN_GZKP)) return NTT_ERR_ARG;  // one rival schedule per plan
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return NTT_ERR_NODEV;
   if (device < 0 || device >= ndev) return NTT_ERR_ARG;

@@ -79,7 +79,7 @@ class NTTPlan:
 
     def __init__(self, field_id: int = 1, log_n: int = 10, limbs64: int = 4, device: int = 0,
                  modulus: Optional[int] = None, generator: Optional[int] = None, twiddle_only: bool = False,
-                 montgomery_io: bool = False, stockham: bool = False):
+                 montgomery_io: bool = False, stockham: bool = False, gzkp: bool = False):
         self._lib = _L.load()
         self.log_n = int(log_n)
         self.n = 1 << self.log_n
@@ -94,6 +94,8 @@ class NTTPlan:
         flags = (_L.NTT_PLAN_TWIDDLE_ONLY if twiddle_only else 0) | (_L.NTT_PLAN_MONTGOMERY_IO if montgomery_io else 0)
         # stockham: forward transforms on the reference's bellperson-family rival schedule (ntt.h)
         flags |= _L.NTT_PLAN_STOCKHAM if stockham else 0
+        # gzkp: the reference's GZKP(B, G) rival schedule (bit reversal + in-place DIT passes)
+        flags |= _L.NTT_PLAN_GZKP if gzkp else 0
         self.montgomery_io = bool(montgomery_io)
         if modulus is None:
             st = self._lib.ntt_plan_create_ex(C.byref(h), int(field_id), self.log_n, self.limbs64, self.device, flags)

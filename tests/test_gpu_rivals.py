@@ -1,8 +1,10 @@
-"""The rival schedule: the reference's bellperson / improved_NTT_v1..v4 family
-(GZKP-NTT.cu:324-386 FIELD_radix_fft, :556-1296) re-derived as Stockham autosort pass kernels
-(KIND_STOCKHAM, plan flag NTT_PLAN_STOCKHAM).  Same contract as the default schedule, so the same
-pins: the reference's own outputs (tests/golden/ref_p469762049.npz) on its field P, the C oracle
-for BN254 Fr, and bit-for-bit agreement with the default four-step DIF schedule."""
+"""The rival schedules, same contract as the default schedule and so the same pins --
+the reference's own outputs (tests/golden/ref_p469762049.npz) on its field P, the C oracle for
+BN254 / BLS12-381 Fr, and bit-for-bit agreement with the default four-step DIF schedule:
+* "stockham": the bellperson / improved_NTT_v1..v4 family (GZKP-NTT.cu:324-386 FIELD_radix_fft,
+  :556-1296) as Stockham autosort pass kernels (KIND_STOCKHAM, plan flag NTT_PLAN_STOCKHAM);
+* "gzkp": GZKP(B, G) (GZKP-NTT.cu:115-233; parallel-load.cu for P): bit reversal, then in-place DIT
+  passes with input twiddles (KIND_DIT, plan flag NTT_PLAN_GZKP)."""
 import os
 
 import numpy as np
@@ -17,16 +19,20 @@ GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "ref_p469762049
 THREADS = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "8"))))
 
 
-def _plan(fid, log_n, L, stockham):
+RIVALS = ["stockham", "gzkp"]
+
+
+def _plan(fid, log_n, L, sched):
     from ntt_amd.ntt import NTTPlan
-    return NTTPlan(field_id=fid, log_n=log_n, limbs64=L, stockham=stockham)
+    return NTTPlan(field_id=fid, log_n=log_n, limbs64=L, stockham=sched == "stockham", gzkp=sched == "gzkp")
 
 
+@pytest.mark.parametrize("sched", RIVALS)
 @pytest.mark.parametrize("log_n", [16, 20, 22, 24, 26])
-def test_stockham_p_path_vs_reference_outputs(log_n):
+def test_rival_p_path_vs_reference_outputs(log_n, sched):
     n = 1 << log_n
     idx = torch.from_numpy(GOLD[f"samp_idx_{log_n}"]).to("cuda:0")
-    pl = _plan(0, log_n, 1, True)
+    pl = _plan(0, log_n, 1, sched)
     t = torch.arange(n, dtype=torch.int64, device="cuda:0")
     pl.forward(t)
     assert np.array_equal(t[idx].cpu().numpy(), GOLD[f"samp_iota_{log_n}"])
@@ -37,12 +43,13 @@ def test_stockham_p_path_vs_reference_outputs(log_n):
     assert np.array_equal(t.cpu().numpy(), OC.random_limbs(0, n, seed=2000 + log_n, L=1)[:, 0].astype(np.int64))
 
 
+@pytest.mark.parametrize("sched", RIVALS)
 @pytest.mark.parametrize("fid,L,log_n", [(0, 1, 14), (0, 1, 18), (1, 4, 11), (1, 4, 13), (1, 4, 16), (2, 4, 17),
                                          (1, 4, 20)])
-def test_stockham_matches_oracle_and_default_schedule(fid, L, log_n):
+def test_rival_matches_oracle_and_default_schedule(fid, L, log_n, sched):
     p, g = R.FIELDS[fid]
-    st = _plan(fid, log_n, L, True)
-    df = _plan(fid, log_n, L, False)
+    st = _plan(fid, log_n, L, sched)
+    df = _plan(fid, log_n, L, "default")
     a = st.fill(st.empty(), "random", seed=log_n)
     b = a.clone()
     x = a.cpu().numpy().view(np.uint64).reshape(-1, L).copy()
@@ -56,10 +63,17 @@ def test_stockham_matches_oracle_and_default_schedule(fid, L, log_n):
         assert np.array_equal(got, OC.ntt_mp(x, p, g))
 
 
-def test_stockham_2pow24_bn254_elementwise():
+@pytest.mark.parametrize("sched", RIVALS)
+def test_rival_2pow24_bn254_elementwise(sched):
     p, g = R.FIELDS[1]
-    st = _plan(1, 24, 4, True)
+    st = _plan(1, 24, 4, sched)
     a = st.fill(st.empty(), "random", seed=24)
     x = a.cpu().numpy().view(np.uint64).reshape(-1, 4).copy()
     st.forward(a)
     assert np.array_equal(a.cpu().numpy().view(np.uint64).reshape(-1, 4), OC.ntt_mp_par(x, p, g, THREADS))
+
+
+def test_rival_flags_are_exclusive():
+    from ntt_amd.ntt import NTTPlan
+    with pytest.raises(Exception):
+        NTTPlan(field_id=1, log_n=12, limbs64=4, stockham=True, gzkp=True)

@@ -1,5 +1,6 @@
-"""Default four-step DIF schedule vs the rival schedule (the reference's bellperson / improved_NTT
-family as Stockham autosort passes, NTT_PLAN_STOCKHAM): forward transforms, inputs in HBM.
+"""Default four-step DIF schedule vs the rival schedules (the reference's bellperson / improved_NTT
+family as Stockham autosort passes, NTT_PLAN_STOCKHAM; GZKP(B, G) as bit reversal + in-place DIT
+passes, NTT_PLAN_GZKP): forward transforms, inputs in HBM.
 
     python tools/bench_rivals.py [--out gpurun_out/rivals.jsonl]
 """
@@ -32,8 +33,8 @@ def main():
     from ntt_amd.ntt import NTTPlan
     rows = []
     for fid, L, lg in ((1, 4, 24), (1, 4, 20), (0, 1, 24), (0, 1, 26)):
-        for sched in ("default", "stockham"):
-            pl = NTTPlan(fid, lg, L, stockham=(sched == "stockham"))
+        for sched in ("default", "stockham", "gzkp"):
+            pl = NTTPlan(fid, lg, L, stockham=(sched == "stockham"), gzkp=(sched == "gzkp"))
             t = pl.fill(pl.empty(), "random", seed=1)
             pl.set_profiling(True)
             s = timeit(lambda: pl.forward(t))
