@@ -286,9 +286,9 @@ class DistNTT:
         self.field_id, self.log_n, self.limbs64 = field_id, log_n, limbs64
         self.layout = Layout(log_n, world, rank)
         self.engine = RankPlan(field_id, log_n, limbs64, world, rank, device)
-        if pieces is None:
-            pieces = self.auto_pieces(self.layout.local_n)
-        self.fs = FourStep(self.layout, self.engine, self, pieces=1 if world == 1 else pieces)
+        if pieces is None:  # world 1: no exchange to hide
+            pieces = 1 if world == 1 else self.auto_pieces(self.layout.local_n)
+        self.fs = FourStep(self.layout, self.engine, self, pieces=pieces)
         self.n = self.layout.n
         self.passes: List[int] = []  # per-transform schedules: see the row / column plans
 

@@ -51,6 +51,8 @@ def test_virtual_ranks_match_single_gpu(world, log_n, field_id, L, pieces):
 
 
 def test_dist_ntt_rccl_world1():
+    """DistNTT over a real RCCL group (world size 1): whole-chunk exchange, and the pipelined
+    exchange (async RCCL all-to-all per row piece, uneven last piece) forced on."""
     import torch.distributed as dist
     from ntt_amd.distributed import DistNTT
     from ntt_amd.ntt import NTTPlan
@@ -59,16 +61,18 @@ def test_dist_ntt_rccl_world1():
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
     try:
         log_n = 16
-        d = DistNTT(1, log_n, 4, device=0)
-        t = d.fill(d.empty(), "random", seed=3)
-        t0 = t.clone()
-        d.forward(t)
         ref = NTTPlan(1, log_n, 4)
         x = ref.fill(ref.empty(), "random", seed=3)
         ref.forward(x)
-        assert torch.equal(t, x[_index(d.layout, "col")])
-        d.inverse(t)
-        assert torch.equal(t, t0)
+        for pieces in (None, 4, 3):
+            d = DistNTT(1, log_n, 4, device=0, pieces=pieces)
+            assert len(d.fs.pieces) == (1 if pieces is None else pieces)
+            t = d.fill(d.empty(), "random", seed=3)
+            t0 = t.clone()
+            d.forward(t)
+            assert torch.equal(t, x[_index(d.layout, "col")]), pieces
+            d.inverse(t)
+            assert torch.equal(t, t0), pieces
     finally:
         dist.destroy_process_group()
 

@@ -121,11 +121,12 @@ def test_dist_ntt_polymul_rccl_world1():
     try:
         log_n = 18
         exp = _single_gpu_product(1, 4, log_n, 5, 6)
-        d = DistNTT(1, log_n, 4, device=0)
-        a = d.fill(d.empty(), "random", seed=5)
-        b = d.fill(d.empty(), "random", seed=6)
-        out = d.empty()
-        d.polymul(a, b, out)
-        assert torch.equal(out, exp[_row_index(d.layout, "cuda:0")])
+        for pieces in (None, 4):  # whole chunks; pipelined async RCCL pieces (a and b in each piece)
+            d = DistNTT(1, log_n, 4, device=0, pieces=pieces)
+            a = d.fill(d.empty(), "random", seed=5)
+            b = d.fill(d.empty(), "random", seed=6)
+            out = d.empty()
+            d.polymul(a, b, out)
+            assert torch.equal(out, exp[_row_index(d.layout, "cuda:0")]), pieces
     finally:
         dist.destroy_process_group()
