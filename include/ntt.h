@@ -189,7 +189,8 @@ int ntt_last_error(void);
  * around the all-to-all, fused so that no separate twiddle, pack or transpose pass runs: the row
  * transforms' last pass applies w_n^(j1 k2) and stores straight into the peer chunks, and the column
  * transforms read the received chunks in place (2^log_c interleaved transforms).  Layouts as the
- * multi-GPU plan below: row layout [r][n2], column layout [n1][c].  Send / receive buffers are the
+ * multi-GPU plan below: row layout [r][n2], column layout [n1][c]; the split n1 x n2 is the plan's
+ * (ntt_rplan_info), the same for every rank of one (field, log_n, limbs64, world).  Send / receive buffers are the
  * caller's: [world][nvec][chunk] elements (chunk = r c, ntt_rplan_info), exchanged by the caller
  * as ONE all-to-all of equal chunks (RCCL, device copies, ...).  nvec = 2 carries two vectors per
  * exchange (polymul: slot 0 = a, slot 1 = b).  All calls are asynchronous on hip_stream. */
@@ -229,8 +230,9 @@ int ntt_rplan_destroy(ntt_rplan* rp);
  * two); a transform is the four-step with ONE RCCL all-to-all over xGMI (ncclCommInitAll over
  * `devices`).  d_data[g] / hip_streams[g] belong to devices[g] (streams may be NULL = default
  * streams); each d_data[g] holds n / ngpus elements.  Device g runs ntt_rplan rank g.  Layouts (as
- * ntt_amd/distributed.py), with
- * n1 = 2^ceil(log_n/2), n2 = 2^floor(log_n/2), r = n1/ngpus, c = n2/ngpus:
+ * ntt_amd/distributed.py), with n = n1 n2, r = n1/ngpus, c = n2/ngpus, where the plan picks the split
+ * (ntt_mplan_info / ntt_rplan_info): the balanced n1 = 2^ceil(log_n/2), n2 = 2^floor(log_n/2) unless
+ * a narrower n2 takes fewer pass kernels (2^24 on the 256-bit engines: n1 = 2^14, n2 = 2^10):
  *   forward input  (row layout):    d_data[g] = [r][n2], element (a, j2) = x[g r + a + n1 j2]
  *   forward output (column layout): d_data[g] = [n1][c], element (k1, kc) = X[g c + kc + n2 k1]
  * The inverse takes the column layout back to the row layout (1/n included).  Asynchronous. */

@@ -26,5 +26,7 @@ int plan_build_fs_table(ntt_plan* plan, void* table, unsigned log_rows, unsigned
                         uint64_t col0, bool inverse, hipStream_t st);
 size_t plan_table_entry_bytes(const ntt_plan* plan);
 int plan_device(const ntt_plan* plan);
+// pass kernels that a 2^log_x-point transform takes with this plan's engine (the four-step split)
+unsigned plan_passes_for(const ntt_plan* plan, unsigned log_x);
 
 }  // namespace ntt

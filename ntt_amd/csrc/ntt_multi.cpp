@@ -2,7 +2,7 @@
 // devices of one node, with the transpose as ONE RCCL all-to-all over xGMI per transform.
 //
 // The layouts are those of ntt_amd/distributed.py (the one-process-per-GPU form of the same
-// schedule): n = n1 n2, n1 = 2^ceil(L/2), n2 = 2^floor(L/2), r = n1 / G rows and c = n2 / G
+// schedule): n = n1 n2 (the rank plans' split, ntt_rplan.cpp choose_split), r = n1 / G rows and c = n2 / G
 // columns per device.
 //   input  (row layout):    device g holds [r][n2], element (a, j2) = x[g r + a + n1 j2]
 //   output (column layout): device g holds [n1][c], element (k1, kc) = X[g c + kc + n2 k1]
@@ -331,11 +331,7 @@ int ntt_mplan_create(ntt_mplan** out, int field_id, unsigned log_n, unsigned lim
   m->ngpus = ngpus;
   m->log_n = log_n;
   m->log_g = (unsigned)__builtin_ctz((unsigned)ngpus);
-  m->log_n1 = (log_n + 1) / 2;
-  m->log_n2 = log_n / 2;
-  if (m->log_g > m->log_n2) { delete m; return NTT_ERR_ARG; }
-  m->log_r = m->log_n1 - m->log_g;
-  m->log_c = m->log_n2 - m->log_g;
+  if (m->log_g > log_n / 2) { delete m; return NTT_ERR_ARG; }
   m->dev.assign(devices, devices + ngpus);
   m->rp.assign(ngpus, nullptr);
   m->send.assign(ngpus, nullptr);
@@ -345,9 +341,13 @@ int ntt_mplan_create(ntt_mplan** out, int field_id, unsigned log_n, unsigned lim
     if (hipSetDevice(devices[g]) != hipSuccess) { rc = NTT_ERR_HIP; break; }
     rc = ntt_rplan_create(&m->rp[g], field_id, log_n, limbs64, ngpus, g, devices[g]);
     if (rc == NTT_OK) {
-      unsigned eb = 0;
-      ntt_rplan_info(m->rp[g], nullptr, nullptr, nullptr, nullptr, &eb);
+      unsigned eb = 0, l1 = 0, l2 = 0;
+      ntt_rplan_info(m->rp[g], nullptr, nullptr, &l1, &l2, &eb);
       m->elem_bytes = eb;
+      m->log_n1 = l1;  // the rank plans' split (the same on every device)
+      m->log_n2 = l2;
+      m->log_r = l1 - m->log_g;
+      m->log_c = l2 - m->log_g;
       if (alloc_pair(m->send, g, m->local_n() * eb) || alloc_pair(m->recv, g, m->local_n() * eb)) rc = NTT_ERR_HIP;
     }
   }

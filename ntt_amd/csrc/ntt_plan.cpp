@@ -98,6 +98,8 @@ struct PlanBase {
   virtual int build_fs_table(void* table, unsigned log_rows, unsigned log_cols, uint64_t row0, uint64_t col0,
                              bool inverse, hipStream_t st) = 0;
   virtual size_t table_entry_bytes() const = 0;
+  // pass kernels a transform of 2^log_x points takes with this plan's engine (its schedule())
+  virtual unsigned passes_for(unsigned log_x) const = 0;
   virtual int coset(void* d, const uint64_t* shift, unsigned limbs64, bool inverse, hipStream_t st) = 0;
   virtual int count_noncanonical(const void* d, uint64_t count, uint64_t* bad, hipStream_t st) = 0;
   uint64_t n = 0;
@@ -840,6 +842,13 @@ struct PlanImpl final : PlanBase {
     return A;
   }
 
+  unsigned passes_for(unsigned log_x) const override {
+    unsigned rr[8] = {0}, p = 0;
+    if (!schedule(log_x, tile_log_of<E>(), E::MIN_COLS_LOG, !E::PASS1_FULL_TABLE && NTT_P_NARROW_FIRST, rr, p))
+      return 99;
+    return p == 0 ? 1 : p;
+  }
+
   int run(void* d, unsigned batch, bool inverse, hipStream_t st) override {
     if (!d || batch == 0 || (flags & NTT_PLAN_TWIDDLE_ONLY)) return NTT_ERR_ARG;
     if ((flags & NTT_PLAN_STOCKHAM) && !inverse && batch == 1 && d_stk_tab)
@@ -1400,4 +1409,7 @@ int plan_build_fs_table(ntt_plan* plan, void* table, unsigned log_rows, unsigned
 }
 size_t plan_table_entry_bytes(const ntt_plan* plan) { return plan && plan->impl ? plan->impl->table_entry_bytes() : 0; }
 int plan_device(const ntt_plan* plan) { return plan && plan->impl ? plan->impl->device : -1; }
+unsigned plan_passes_for(const ntt_plan* plan, unsigned log_x) {
+  return plan && plan->impl ? plan->impl->passes_for(log_x) : 99u;
+}
 }  // namespace ntt

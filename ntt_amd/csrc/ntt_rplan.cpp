@@ -1,8 +1,9 @@
 // One rank of the distributed four-step NTT: the local steps around the all-to-all,
 // fused so that no separate twiddle, pack or transpose pass touches HBM.
 //
-//   n = n1 n2, n1 = 2^ceil(L/2), n2 = 2^floor(L/2); rank g of G owns r = n1/G rows and c = n2/G
-//   columns.  Layouts (ntt.h):
+//   n = n1 n2 with n1 >= n2: the balanced split n1 = 2^ceil(L/2), n2 = 2^floor(L/2) unless a narrower
+//   n2 needs fewer pass kernels in total (choose_split; ntt_rplan_info reports it); rank g of G owns
+//   r = n1/G rows and c = n2/G columns.  Layouts (ntt.h):
 //     row layout     [r][n2]: local (a, j2)  = x[g r + a + n1 j2]
 //     column layout  [n1][c]: local (k1, kc) = X[g c + kc + n2 k1]   (transform index fastest)
 //
@@ -19,6 +20,8 @@
 // The buffers are the caller's ([G][nvec][r c] elements each), so the exchange can be RCCL through
 // torch.distributed, ncclAllToAll in ntt_mplan, or device copies between virtual ranks.
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 
 #include "../../include/ntt.h"
 #include "ntt_internal.hpp"
@@ -65,6 +68,30 @@ hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
 
 bool nvec_ok(unsigned nvec, unsigned slot) { return (nvec == 1 || nvec == 2) && slot < nvec; }
 
+// The split n = n1 n2 (log_n2 returned): fewest pass kernels over the row (length n2) and column
+// (length n1) transforms, the most balanced split among equals.  2^24 on the 256-bit engines: 12 + 12
+// takes 2 + 2 passes, 14 + 10 takes 2 + 1 (the rows one workgroup tile each) -- as many HBM passes
+// as the one-GPU transform; 2^28 stays 14 + 14 (4 passes either way).
+unsigned choose_split(const ntt_plan* tw, unsigned log_n, unsigned log_g) {
+  const unsigned bal = log_n / 2;
+  if (const char* e = std::getenv("NTT_FS_LOG_N2")) {  // experiments (tools/ab_env.sh): a fixed n2
+    const unsigned v = (unsigned)std::atoi(e);
+    if (v >= 3 && v >= log_g && v <= bal) return v;
+  }
+  unsigned best = bal, best_p = ~0u;
+  for (unsigned s2 = bal; s2 >= 3 && s2 >= log_g; --s2) {
+    const unsigned p = plan_passes_for(tw, log_n - s2) + plan_passes_for(tw, s2);
+    if (p < best_p) {
+      best_p = p;
+      best = s2;
+    }
+  }
+  return best;
+}
+
+// grid.y of a row launch is its row count: launches of at most 2^15 rows
+constexpr uint64_t kMaxRowsPerLaunch = 1ull << 15;
+
 // a row piece [row0, row0 + nrows) of the r local rows
 bool range_ok(const ntt_rplan* rp, uint64_t row0, uint64_t nrows) {
   const uint64_t r = 1ull << rp->log_r;
@@ -86,19 +113,21 @@ int ntt_rplan_create(ntt_rplan** out, int field_id, unsigned log_n, unsigned lim
   rp->device = device;
   rp->log_n = log_n;
   rp->log_g = (unsigned)__builtin_ctz((unsigned)world);
-  rp->log_n1 = (log_n + 1) / 2;
-  rp->log_n2 = log_n / 2;
   // every local transform has >= 8 points (one or more pass kernels) and >= 1 row / column per rank
-  if (rp->log_n2 < 3 || rp->log_g > rp->log_n2) {
+  if (log_n / 2 < 3 || rp->log_g > log_n / 2) {
     delete rp;
     return NTT_ERR_ARG;
   }
-  rp->log_r = rp->log_n1 - rp->log_g;
-  rp->log_c = rp->log_n2 - rp->log_g;
   DeviceScope scope(device);
-  int rc = ntt_plan_create(&rp->rows, field_id, rp->log_n2, limbs64, device);
+  int rc = ntt_plan_create_ex(&rp->tw, field_id, log_n, limbs64, device, NTT_PLAN_TWIDDLE_ONLY);
+  if (rc == NTT_OK) {
+    rp->log_n2 = choose_split(rp->tw, log_n, rp->log_g);
+    rp->log_n1 = log_n - rp->log_n2;
+    rp->log_r = rp->log_n1 - rp->log_g;
+    rp->log_c = rp->log_n2 - rp->log_g;
+    rc = ntt_plan_create(&rp->rows, field_id, rp->log_n2, limbs64, device);
+  }
   if (rc == NTT_OK) rc = ntt_plan_create(&rp->cols, field_id, rp->log_n1, limbs64, device);
-  if (rc == NTT_OK) rc = ntt_plan_create_ex(&rp->tw, field_id, log_n, limbs64, device, NTT_PLAN_TWIDDLE_ONLY);
   if (rc == NTT_OK) {
     uint64_t n = 0;
     unsigned eb = 0;
@@ -138,6 +167,13 @@ int ntt_rplan_info(const ntt_rplan* rp, uint64_t* local_n, uint64_t* chunk, unsi
 int ntt_rplan_forward_rows_range(ntt_rplan* rp, const void* d_x, void* d_send, unsigned nvec, unsigned slot,
                                  uint64_t row0, uint64_t nrows, void* s) {
   if (!rp || !d_x || !d_send || !nvec_ok(nvec, slot) || !range_ok(rp, row0, nrows)) return NTT_ERR_ARG;
+  if (nrows > kMaxRowsPerLaunch) {
+    for (uint64_t a = 0; a < nrows; a += kMaxRowsPerLaunch) {
+      const uint64_t m = nrows - a < kMaxRowsPerLaunch ? nrows - a : kMaxRowsPerLaunch;
+      if (int rc = ntt_rplan_forward_rows_range(rp, d_x, d_send, nvec, slot, row0 + a, m, s)) return rc;
+    }
+    return NTT_OK;
+  }
   DeviceScope scope(rp->device);
   // batch index b of the launch is local row row0 + b: shift the input rows, the epilogue table rows
   // and the Mode B output map (row a lands at a c within every peer chunk) by row0
@@ -181,6 +217,13 @@ int ntt_rplan_inverse_cols(ntt_rplan* rp, const void* d_x, const void* d_y, void
 int ntt_rplan_inverse_rows_range(ntt_rplan* rp, const void* d_recv, void* d_out, uint64_t row0, uint64_t nrows,
                                  void* s) {
   if (!rp || !d_recv || !d_out || !range_ok(rp, row0, nrows)) return NTT_ERR_ARG;
+  if (nrows > kMaxRowsPerLaunch) {
+    for (uint64_t a = 0; a < nrows; a += kMaxRowsPerLaunch) {
+      const uint64_t m = nrows - a < kMaxRowsPerLaunch ? nrows - a : kMaxRowsPerLaunch;
+      if (int rc = ntt_rplan_inverse_rows_range(rp, d_recv, d_out, row0 + a, m, s)) return rc;
+    }
+    return NTT_OK;
+  }
   DeviceScope scope(rp->device);
   FsIO io;
   io.fs = FS_MAP_IN;

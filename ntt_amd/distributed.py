@@ -1,6 +1,6 @@
 """Multi-GPU NTT: four-step decomposition with one all-to-all.
 
-n = n1 * n2, j = j1 + n1*j2, k = k2 + n2*k1:
+n = n1 * n2 (n1 >= n2; the rank plan picks the split, Layout), j = j1 + n1*j2, k = k2 + n2*k1:
 
     X[k2 + n2 k1] = sum_j1 w_n1^(j1 k1) * w_n^(j1 k2) * sum_j2 w_n2^(j2 k2) x[j1 + n1 j2]
 
@@ -36,16 +36,23 @@ import torch
 
 @dataclass
 class Layout:
+    """n = n1 n2 over ``world`` ranks.  ``log_n2`` None: the balanced split (n2 = 2^floor(L/2)); the
+    rank plans pick their own (ntt_rplan_info: balanced unless a narrower n2 takes fewer passes) and
+    pass it here."""
     log_n: int
     world: int
     rank: int
+    log_n2: Optional[int] = None
 
     def __post_init__(self):
         if self.world < 1 or self.world & (self.world - 1):
             raise ValueError("world size must be a power of two")
         self.log_g = self.world.bit_length() - 1
-        self.log_n1 = (self.log_n + 1) // 2
-        self.log_n2 = self.log_n // 2
+        if self.log_n2 is None:
+            self.log_n2 = self.log_n // 2
+        self.log_n1 = self.log_n - self.log_n2
+        if self.log_n2 > self.log_n1 or self.log_n2 < 0:
+            raise ValueError(f"bad split 2^{self.log_n1} x 2^{self.log_n2}")
         if self.log_g > self.log_n2:
             raise ValueError(f"2^{self.log_n} is too small to split over {self.world} ranks")
         self.log_r = self.log_n1 - self.log_g  # local rows (row layout)
@@ -192,7 +199,9 @@ class RankPlan:
         _L.check(self.lib.ntt_rplan_create(C.byref(h), field_id, log_n, limbs64, world, rank, device),
                  "ntt_rplan_create")
         self.handle = h
-        self.layout = Layout(log_n, world, rank)
+        n1, n2 = C.c_uint(), C.c_uint()
+        _L.check(self.lib.ntt_rplan_info(h, None, None, C.byref(n1), C.byref(n2), None), "ntt_rplan_info")
+        self.layout = Layout(log_n, world, rank, n2.value)
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -284,8 +293,8 @@ class DistNTT:
             device = torch.cuda.current_device()
         self.device = device
         self.field_id, self.log_n, self.limbs64 = field_id, log_n, limbs64
-        self.layout = Layout(log_n, world, rank)
         self.engine = RankPlan(field_id, log_n, limbs64, world, rank, device)
+        self.layout = self.engine.layout
         if pieces is None:  # world 1: no exchange to hide
             pieces = 1 if world == 1 else self.auto_pieces(self.layout.local_n)
         self.fs = FourStep(self.layout, self.engine, self, pieces=pieces)
@@ -359,7 +368,7 @@ class VirtualRanks:
     def __init__(self, field_id: int, log_n: int, limbs64: int, world: int, device: int = 0, pieces: int = 1):
         self.world = world
         self.engines = [RankPlan(field_id, log_n, limbs64, world, g, device) for g in range(world)]
-        self.ranks = [FourStep(Layout(log_n, world, g), e, pieces=pieces) for g, e in enumerate(self.engines)]
+        self.ranks = [FourStep(e.layout, e, pieces=pieces) for e in self.engines]
         self.layout0 = self.ranks[0].L
         self.pieces = self.ranks[0].pieces
         self.side = torch.cuda.Stream(device=device)
@@ -462,7 +471,7 @@ class MultiPlan:
         local_n, n1, n2 = C.c_uint64(), C.c_uint(), C.c_uint()
         self.lib.ntt_mplan_info(h, C.byref(local_n), C.byref(n1), C.byref(n2))
         self.local_n, self.log_n1, self.log_n2 = local_n.value, n1.value, n2.value
-        self.layouts = [Layout(log_n, len(self.devices), g) for g in range(len(self.devices))]
+        self.layouts = [Layout(log_n, len(self.devices), g, self.log_n2) for g in range(len(self.devices))]
         if pieces is not None:
             _L.check(self.lib.ntt_mplan_set_pieces(h, int(pieces)), "ntt_mplan_set_pieces")
 

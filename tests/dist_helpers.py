@@ -14,11 +14,11 @@ from oracle import oracle_c as OC
 
 
 class CpuOracleEngine:
-    def __init__(self, field_id, log_n, limbs64, world=1, rank=0):
+    def __init__(self, field_id, log_n, limbs64, world=1, rank=0, log_n2=None):
         from ntt_amd.distributed import Layout
         self.p, self.g = R.FIELDS[field_id]
         self.L = limbs64
-        self.lay = Layout(log_n, world, rank)
+        self.lay = Layout(log_n, world, rank, log_n2)
         n = 1 << log_n
         w = R.root_of_unity(self.p, self.g, n)
         self.w, self.winv, self.n = w, pow(w, self.p - 2, self.p), n
@@ -110,21 +110,21 @@ class GlooPieceExchange:
         pass
 
 
-def row_shares(x_ints, layout_cls, log_n, world, L):
+def row_shares(x_ints, layout_cls, log_n, world, L, log_n2=None):
     """Split a global vector into the row-layout shares of every rank (limb arrays)."""
     shares = []
     for g in range(world):
-        lay = layout_cls(log_n, world, g)
+        lay = layout_cls(log_n, world, g, log_n2)
         vals = [x_ints[lay.row_global(i)] for i in range(lay.local_n)]
         shares.append(torch.from_numpy(OC.ints_to_limbs(vals, L).view(np.int64)))
     return shares
 
 
-def gather_cols(shares, layout_cls, log_n, world, L):
+def gather_cols(shares, layout_cls, log_n, world, L, log_n2=None):
     n = 1 << log_n
     X = [None] * n
     for g, t in enumerate(shares):
-        lay = layout_cls(log_n, world, g)
+        lay = layout_cls(log_n, world, g, log_n2)
         vals = OC.limbs_to_ints(t.numpy().view(np.uint64).reshape(-1, L))
         for i, v in enumerate(vals):
             X[lay.col_global(i)] = v

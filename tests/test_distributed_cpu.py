@@ -29,7 +29,7 @@ def _exchange(layout, pieces):
     return GlooPieceExchange(layout)
 
 
-def _worker(rank, world, port, field_id, log_n, L, q, pieces=1):
+def _worker(rank, world, port, field_id, log_n, L, q, pieces=1, log_n2=None):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from ntt_amd.distributed import FourStep, Layout
@@ -40,34 +40,37 @@ def _worker(rank, world, port, field_id, log_n, L, q, pieces=1):
     try:
         n = 1 << log_n
         x = R.random_vector(field_id, n, seed=77)
-        share = row_shares(x, Layout, log_n, world, L)[rank]
-        eng = CpuOracleEngine(field_id, log_n, L, world, rank)
-        lay = Layout(log_n, world, rank)
+        share = row_shares(x, Layout, log_n, world, L, log_n2)[rank]
+        eng = CpuOracleEngine(field_id, log_n, L, world, rank, log_n2)
+        lay = Layout(log_n, world, rank, log_n2)
         fs = FourStep(lay, eng, _exchange(lay, pieces), pieces=pieces)
         assert len(fs.pieces) == min(pieces, lay.r)
         fs.forward(share)
         fwd = share.clone()
         fs.inverse(share)
         back = OC.limbs_to_ints(share.numpy().view("uint64").reshape(-1, L))
-        lay = Layout(log_n, world, rank)
         ok_rt = back == [x[lay.row_global(i)] for i in range(lay.local_n)]
         q.put((rank, fwd.numpy().tobytes(), ok_rt))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,field_id,log_n,pieces", [(2, 1, 6, 1), (2, 2, 7, 1), (4, 1, 8, 1), (2, 1, 6, 2),
-                                                          (2, 2, 7, 3), (4, 1, 8, 4)])
-def test_four_step_gloo(world, field_id, log_n, pieces):
+@pytest.mark.parametrize("world,field_id,log_n,pieces,log_n2", [(2, 1, 6, 1, None), (2, 2, 7, 1, None),
+                                                                 (4, 1, 8, 1, None), (2, 1, 6, 2, None),
+                                                                 (2, 2, 7, 3, None), (4, 1, 8, 4, None),
+                                                                 (2, 1, 8, 2, 3), (4, 2, 9, 1, 3)])
+def test_four_step_gloo(world, field_id, log_n, pieces, log_n2):
     """pieces > 1: the pipelined schedule (row transforms and the all-to-all in row pieces, uneven
-    last piece included) gives the same column layout and round trip."""
+    last piece included) gives the same column layout and round trip.  log_n2: an unbalanced split
+    n1 > n2 (what the rank plans pick when it saves a pass, ntt_rplan.cpp choose_split)."""
     from ntt_amd.distributed import Layout
     from tests.dist_helpers import gather_cols
     L = 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, field_id, log_n, L, q, pieces)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, field_id, log_n, L, q, pieces, log_n2))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -79,7 +82,7 @@ def test_four_step_gloo(world, field_id, log_n, pieces):
         assert p.exitcode == 0
     import numpy as np
     shares = [torch.from_numpy(np.frombuffer(res[r][0], dtype=np.int64).copy().reshape(-1, L)) for r in range(world)]
-    X = gather_cols(shares, Layout, log_n, world, L)
+    X = gather_cols(shares, Layout, log_n, world, L, log_n2)
     p_, g_ = R.FIELDS[field_id]
     x = R.random_vector(field_id, 1 << log_n, seed=77)
     assert X == R.ntt_dit(x, p_, g_)
@@ -88,12 +91,11 @@ def test_four_step_gloo(world, field_id, log_n, pieces):
 
 def test_layout_index_maps_are_bijections():
     from ntt_amd.distributed import Layout
-    for log_n, world in ((6, 2), (9, 4), (12, 8)):
+    for log_n, world, log_n2 in ((6, 2, None), (9, 4, None), (12, 8, None), (12, 2, 4), (11, 4, 2)):
         n = 1 << log_n
-        rows = sorted(Layout(log_n, world, g).row_global(i) for g in range(world)
-                      for i in range(Layout(log_n, world, g).local_n))
-        cols = sorted(Layout(log_n, world, g).col_global(i) for g in range(world)
-                      for i in range(Layout(log_n, world, g).local_n))
+        lays = [Layout(log_n, world, g, log_n2) for g in range(world)]
+        rows = sorted(lay.row_global(i) for lay in lays for i in range(lay.local_n))
+        cols = sorted(lay.col_global(i) for lay in lays for i in range(lay.local_n))
         assert rows == list(range(n)) and cols == list(range(n))
 
 
@@ -103,9 +105,13 @@ def test_layout_rejects_bad_world():
         Layout(10, 3, 0)
     with pytest.raises(ValueError):
         Layout(4, 8, 0)
+    with pytest.raises(ValueError):
+        Layout(10, 2, 0, 6)  # n2 > n1
+    with pytest.raises(ValueError):
+        Layout(10, 8, 0, 2)  # fewer columns than ranks
 
 
-def _polymul_worker(rank, world, port, field_id, log_n, L, square, q, pieces=1):
+def _polymul_worker(rank, world, port, field_id, log_n, L, square, q, pieces=1, log_n2=None):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from ntt_amd.distributed import FourStep, Layout
@@ -117,11 +123,11 @@ def _polymul_worker(rank, world, port, field_id, log_n, L, square, q, pieces=1):
         n = 1 << log_n
         a = R.random_vector(field_id, n, seed=5)
         b = a if square else R.random_vector(field_id, n, seed=6)
-        sa = row_shares(a, Layout, log_n, world, L)[rank]
-        sb = sa if square else row_shares(b, Layout, log_n, world, L)[rank]
+        sa = row_shares(a, Layout, log_n, world, L, log_n2)[rank]
+        sb = sa if square else row_shares(b, Layout, log_n, world, L, log_n2)[rank]
         out = torch.zeros_like(sa)
-        eng = CpuOracleEngine(field_id, log_n, L, world, rank)
-        lay = Layout(log_n, world, rank)
+        eng = CpuOracleEngine(field_id, log_n, L, world, rank, log_n2)
+        lay = Layout(log_n, world, rank, log_n2)
         fs = FourStep(lay, eng, _exchange(lay, pieces), pieces=pieces)
         fs.polymul(sa, sb, out)
         q.put((rank, out.numpy().tobytes()))
@@ -129,10 +135,14 @@ def _polymul_worker(rank, world, port, field_id, log_n, L, square, q, pieces=1):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,field_id,log_n,square,pieces", [(2, 1, 6, False, 1), (4, 1, 8, False, 1),
-                                                                 (2, 2, 7, True, 1), (2, 1, 6, False, 2),
-                                                                 (4, 1, 8, False, 4), (2, 2, 7, True, 2)])
-def test_distributed_polymul_gloo(world, field_id, log_n, square, pieces):
+@pytest.mark.parametrize("world,field_id,log_n,square,pieces,log_n2", [(2, 1, 6, False, 1, None),
+                                                                        (4, 1, 8, False, 1, None),
+                                                                        (2, 2, 7, True, 1, None),
+                                                                        (2, 1, 6, False, 2, None),
+                                                                        (4, 1, 8, False, 4, None),
+                                                                        (2, 2, 7, True, 2, None),
+                                                                        (2, 1, 8, False, 2, 3)])
+def test_distributed_polymul_gloo(world, field_id, log_n, square, pieces, log_n2):
     """C5's schedule (forward(a), forward(b) in ONE all-to-all, local pointwise product fused into
     the inverse, inverse all-to-all) over gloo: the row-layout result equals the oracle's cyclic
     product; squaring (a is b) takes the single-vector exchange."""
@@ -142,7 +152,7 @@ def test_distributed_polymul_gloo(world, field_id, log_n, square, pieces):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_polymul_worker, args=(r, world, port, field_id, log_n, L, square, q, pieces))
+    procs = [ctx.Process(target=_polymul_worker, args=(r, world, port, field_id, log_n, L, square, q, pieces, log_n2))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -160,7 +170,7 @@ def test_distributed_polymul_gloo(world, field_id, log_n, square, pieces):
     exp = R.polymul(a, b, p_, g_)
     got = [None] * n
     for r in range(world):
-        lay = Layout(log_n, world, r)
+        lay = Layout(log_n, world, r, log_n2)
         vals = OC.limbs_to_ints(np.frombuffer(res[r], dtype=np.uint64).reshape(-1, L))
         for i, v in enumerate(vals):
             got[lay.row_global(i)] = v

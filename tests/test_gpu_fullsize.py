@@ -78,6 +78,7 @@ def test_c4_fourstep_2pow28_eight_virtual_ranks():
     p, g = R.FIELDS[fid]
     n = 1 << log_n
     vr = VirtualRanks(fid, log_n, L, world, pieces=4)  # the pipelined exchange, as timed in bench_configs
+    assert (vr.layout0.log_n1, vr.layout0.log_n2) == (14, 14)  # SURVEY §8e's C4 split (4 passes either way)
     xs = vr.fill(vr.empty(), "iota")
     vr.forward(xs)
     rng = np.random.default_rng(4)
