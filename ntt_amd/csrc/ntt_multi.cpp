@@ -276,8 +276,12 @@ int forward_vectors(ntt_mplan* m, void* const* const* v, int nv, void* const* st
       if (int rc = exchange_rows(m, sb, rb, nv, a0, ra)) return rc;
       if (int rc = record_piece(m, i)) return rc;
     }
-    for (unsigned i = 0; i < m->pieces; ++i)
+    for (unsigned i = 0; i < m->pieces; ++i) {  // only the pieces exchanged above (a short last one ends it)
+      size_t a0, ra;
+      piece_range(m, i, a0, ra);
+      if (ra == 0) break;
       if (int rc = order_compute_after_piece(m, streams, i)) return rc;
+    }
   }
   for (int g = 0; g < m->ngpus; ++g)
     for (int k = 0; k < nv; ++k)
