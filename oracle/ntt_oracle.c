@@ -15,6 +15,9 @@
  *                      explicit to/from conversion, mirroring bn2mont/mont_mul/mont2bn
  *                      (impl_cuda.cu:980-1024) semantically.
  *   inverse          — GZKP-NTT.cu:1725-1732: forward with inv(root), then multiply by inv(n).
+ *   oracle_eval_random_mp — the definition X_k = sum_j x_j w^(jk) (GZKP-NTT.cu:30-48) evaluated
+ *                      directly at sampled k for SURVEY §8d's synthetic vector B generated on the
+ *                      fly: spot checks of 2^28 transforms (C4) without an FFT or an 8-GiB copy.
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -357,5 +360,94 @@ int oracle_mul_mp(uint64_t* c, const uint64_t* a, const uint64_t* b, uint64_t n,
     mp_to_mont(am, a + i * L, &F);
     mp_montmul(c + i * L, am, b + i * L, &F);
   }
+  return 0;
+}
+
+/* ------------------------------------------------------------------ sampled outputs at full size
+ * X_k = sum_j x_j w^(jk), w = g^((p-1)/n), of SURVEY §8d's synthetic vector B -- limb i of x_j is
+ * SplitMix64(seed 2^32 + 4j + i) for i < nrand, the last of them masked to top_bits, higher limbs 0
+ * (generated on the fly: a 2^28 vector is never stored) -- at `count` indices ks[].  The definition
+ * of GZKP-NTT.cu:30-48 evaluated directly (no FFT): Horner over `nch` chunks of j split across
+ * `threads` OpenMP threads, chunk c contributing w^(k j0_c) * sum_{j in c} x_j w^(k (j - j0_c)).
+ * out: count elements of limbs64 canonical limbs.  Test infrastructure (C4 spot checks). */
+static uint64_t splitmix_limb(uint64_t seed, uint64_t j, uint32_t i) {
+  uint64_t z = (seed << 32) + 4 * j + i + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+/* mp_montmul / mp_addmod with the limb count fixed at compile time (the compiler unrolls them): the
+ * evaluator's inner loop, 2^28 iterations per sample at C4 */
+#define MP_FIXED(NL)                                                                                   \
+  static void montmul_##NL(uint64_t* r, const uint64_t* a, const uint64_t* b, const mp_field* F) {    \
+    uint64_t t[NL + 2] = {0};                                                                          \
+    for (int i = 0; i < NL; i++) {                                                                     \
+      u128 c = 0;                                                                                      \
+      for (int j = 0; j < NL; j++) { c += (u128)a[j] * b[i] + t[j]; t[j] = (uint64_t)c; c >>= 64; }   \
+      c += t[NL]; t[NL] = (uint64_t)c; t[NL + 1] = (uint64_t)(c >> 64);                                \
+      uint64_t m = t[0] * F->pinv;                                                                     \
+      c = (u128)m * F->p[0] + t[0];                                                                    \
+      c >>= 64;                                                                                        \
+      for (int j = 1; j < NL; j++) { c += (u128)m * F->p[j] + t[j]; t[j - 1] = (uint64_t)c; c >>= 64; } \
+      c += t[NL]; t[NL - 1] = (uint64_t)c; t[NL] = t[NL + 1] + (uint64_t)(c >> 64);                    \
+    }                                                                                                  \
+    if (t[NL] || mp_cmp(t, F->p, NL) >= 0) mp_sub(t, t, F->p, NL);                                     \
+    memcpy(r, t, 8 * NL);                                                                              \
+  }
+MP_FIXED(1)
+MP_FIXED(4)
+MP_FIXED(6)
+
+typedef void (*montmul_fn)(uint64_t*, const uint64_t*, const uint64_t*, const mp_field*);
+
+int oracle_eval_random_mp(uint64_t* out, const uint64_t* ks, uint32_t count, uint32_t log_n, uint32_t limbs64,
+                          const uint64_t* p, const uint64_t* g, uint64_t seed, uint32_t nrand, uint32_t top_bits,
+                          int threads) {
+  mp_field F;
+  if (mp_field_init(&F, p, (int)limbs64) || nrand < 1 || nrand > limbs64 || top_bits > 64) return -1;
+  const int L = F.L;
+  const uint64_t n = 1ull << log_n;
+  if (threads < 1) threads = 1;
+  uint64_t nch = 1; /* a power of two, so that chunks tile [0, n) */
+  while (nch * 2 <= (uint64_t)threads * 4 && nch * 2 <= n) nch *= 2;
+  const uint64_t len = n / nch;
+  uint64_t pm1[MAXL], one[MAXL] = {1}, gm[MAXL], e[MAXL] = {0}, wm[MAXL];
+  mp_sub(pm1, p, one, L);
+  for (int i = 0; i < L; i++) {
+    e[i] = log_n < 64 ? pm1[i] >> log_n : 0;
+    if (i + 1 < L && log_n && log_n < 64) e[i] |= pm1[i + 1] << (64 - log_n);
+  }
+  mp_to_mont(gm, g, &F);
+  mp_pow_mont(wm, gm, e, &F); /* w, Montgomery form */
+  uint64_t* part = (uint64_t*)calloc((size_t)count * nch * L, 8);
+  if (!part) return -1;
+  const uint64_t mask = top_bits >= 64 ? ~0ull : ((1ull << top_bits) - 1);
+  const montmul_fn mm = L == 4 ? montmul_4 : (L == 6 ? montmul_6 : (L == 1 ? montmul_1 : mp_montmul));
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1)
+  for (uint64_t task = 0; task < (uint64_t)count * nch; task++) {
+    const uint64_t s = task / nch, c = task % nch, j0 = c * len;
+    uint64_t kk[MAXL] = {0}, wk[MAXL], acc[MAXL] = {0}, x[MAXL], sh[MAXL];
+    kk[0] = ks[s] & (n - 1);
+    mp_pow_mont(wk, wm, kk, &F); /* w^k, Montgomery form */
+    for (uint64_t j = j0 + len; j-- > j0;) {
+      mm(acc, acc, wk, &F); /* canonical acc times w^k */
+      memset(x, 0, sizeof(x));
+      for (uint32_t i = 0; i < nrand; i++) x[i] = splitmix_limb(seed, j, i);
+      x[nrand - 1] &= mask;
+      mp_addmod(acc, acc, x, &F);
+    }
+    uint64_t ej[MAXL] = {0};
+    /* w^(k j0): exponent k j0 mod n (w has order n) */
+    ej[0] = (kk[0] * j0) & (n - 1);
+    mp_pow_mont(sh, wm, ej, &F);
+    mp_montmul(part + (s * nch + c) * L, acc, sh, &F);
+  }
+  for (uint32_t s = 0; s < count; s++) {
+    uint64_t tot[MAXL] = {0};
+    for (uint64_t c = 0; c < nch; c++) mp_addmod(tot, tot, part + (s * nch + c) * L, &F);
+    memcpy(out + (size_t)s * L, tot, 8 * L);
+  }
+  free(part);
   return 0;
 }

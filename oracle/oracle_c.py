@@ -40,6 +40,9 @@ def load() -> C.CDLL:
                                           C.c_int]
         lib.oracle_mul_mp.restype = C.c_int
         lib.oracle_mul_mp.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]
+        lib.oracle_eval_random_mp.restype = C.c_int
+        lib.oracle_eval_random_mp.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                              C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int]
         _lib = lib
     return _lib
 
@@ -96,6 +99,24 @@ def mul_mp(a: np.ndarray, b: np.ndarray, p: int) -> np.ndarray:
     return c
 
 
+RANDOM_SHAPE = {0: (1, 28), 1: (4, 61), 2: (4, 62)}  # field_id -> (random limbs, bits of the top one)
+
+
+def eval_random(field_id: int, log_n: int, seed: int, ks, L: int, threads: int = 1):
+    """X_k of the forward transform of vector B (random_limbs(field_id, 2^log_n, seed, L)) at the
+    indices ks, from the definition (oracle_eval_random_mp); returns Python ints."""
+    from oracle import ntt_ref as R
+    p, g = R.FIELDS[field_id]
+    nrand, top = RANDOM_SHAPE[field_id]
+    karr = np.ascontiguousarray(np.asarray(ks, dtype=np.uint64))
+    out = np.zeros((len(karr), L), dtype=np.uint64)
+    pl, gl = _limbs(p, L), _limbs(g, L)
+    rc = load().oracle_eval_random_mp(out.ctypes.data, karr.ctypes.data, len(karr), log_n, L, pl.ctypes.data,
+                                      gl.ctypes.data, seed, nrand, top, int(threads))
+    assert rc == 0
+    return limbs_to_ints(out)
+
+
 def ints_to_limbs(values, L: int) -> np.ndarray:
     out = np.zeros((len(values), L), dtype=np.uint64)
     for j, v in enumerate(values):
@@ -118,7 +139,7 @@ def random_limbs(field_id: int, n: int, seed: int, L: int) -> np.ndarray:
     """Vectorised SURVEY §8d vector B (same values as ntt_ref.random_vector), as [n, L] limbs."""
     j = np.arange(n, dtype=np.uint64)
     out = np.zeros((n, L), dtype=np.uint64)
-    nrand, top = {0: (1, 28), 1: (4, 61), 2: (4, 62)}[field_id]
+    nrand, top = RANDOM_SHAPE[field_id]
     with np.errstate(over="ignore"):
         for i in range(min(nrand, L)):
             c = (np.uint64(seed) << np.uint64(32)) + np.uint64(4) * j + np.uint64(i)

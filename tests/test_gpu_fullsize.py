@@ -5,7 +5,11 @@
   headline), BLS12-381 Fr forward and inverse in the 6 x 64-bit layout (C3), the 8-B P path at 2^26;
 * C4's four-step at 2^28 over 8 virtual ranks (one GPU, exchange = device copies): the closed-form
   KAT of x_j = j at sampled k of the gathered column layout, plus the inverse round trip;
-* the single-process multi-GPU plan (ntt_mplan_*, RCCL) at 2^26 and 2^28 on the visible devices.
+* the single-process multi-GPU plan (ntt_mplan_*, RCCL) at 2^26 and 2^28 on the visible devices;
+* C4 at 2^28 on SURVEY §8d's random vector B (seed 4), both as the plain one-GPU transform and as the
+  four-step over 8 virtual ranks: sampled outputs against the definition evaluated directly on the
+  CPU (oracle_eval_random_mp, Horner over the on-the-fly generated vector; pinned against the
+  oracle's NTT in test_oracle.py).
 """
 import os
 
@@ -105,3 +109,35 @@ def test_mplan_large_kat_and_round_trip(log_n):
     for lay, t in zip(mp.layouts, xs):
         assert torch.equal(t[:, 0], _row_index(lay, t.device)) and not bool(t[:, 1:].any())
     del mp
+
+
+C4_SEED = 4
+C4_KS = [1, 0x5A5A5A5, (1 << 28) - 3]  # a low, a scattered and a top index (~4 s each on 16 cores)
+
+
+@pytest.fixture(scope="module")
+def c4_expected():
+    return OC.eval_random(1, 28, C4_SEED, C4_KS, 4, threads=THREADS)
+
+
+def test_c4_random_2pow28_plain_sampled_vs_definition(c4_expected):
+    pl = _plan(1, 28, 4)
+    t = pl.fill(pl.empty(), "random", seed=C4_SEED)
+    pl.forward(t)
+    got = OC.limbs_to_ints(_host(t[C4_KS], 4))
+    assert got == c4_expected
+    del t, pl
+
+
+def test_c4_random_2pow28_fourstep_sampled_vs_definition(c4_expected):
+    from ntt_amd.distributed import VirtualRanks
+    vr = VirtualRanks(1, 28, 4, 8, pieces=4)
+    xs = vr.fill(vr.empty(), "random", seed=C4_SEED)
+    vr.forward(xs)
+    L0 = vr.layout0
+    got = []
+    for k in C4_KS:
+        k2, k1 = k % L0.n2, k // L0.n2
+        rank, kc = k2 // L0.c, k2 % L0.c
+        got.append(OC.limbs_to_ints(_host(xs[rank][k1 * L0.c + kc].reshape(1, 4), 4))[0])
+    assert got == c4_expected
