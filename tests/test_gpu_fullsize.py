@@ -6,6 +6,7 @@
 * C4's four-step at 2^28 over 8 virtual ranks (one GPU, exchange = device copies): the closed-form
   KAT of x_j = j at sampled k of the gathered column layout, plus the inverse round trip;
 * the single-process multi-GPU plan (ntt_mplan_*, RCCL) at 2^26 and 2^28 on the visible devices;
+* C5's polymul at 2^24 (degree < 2^23 inputs from vector B, seeds 5 and 6), element by element;
 * C4 at 2^28 on SURVEY §8d's random vector B (seed 4), both as the plain one-GPU transform and as the
   four-step over 8 virtual ranks: sampled outputs against the definition evaluated directly on the
   CPU (oracle_eval_random_mp, Horner over the on-the-fly generated vector; pinned against the
@@ -109,6 +110,30 @@ def test_mplan_large_kat_and_round_trip(log_n):
     for lay, t in zip(mp.layouts, xs):
         assert torch.equal(t[:, 0], _row_index(lay, t.device)) and not bool(t[:, 1:].any())
     del mp
+
+
+def test_c5_polymul_2pow24_elementwise_vs_threaded_oracle():
+    """C5: a, b of degree < 2^23 drawn from vector B (seeds 5 and 6), c = a * b of
+    length 2^24 by the fused ntt_polymul, every coefficient against the oracle's forward transforms,
+    pointwise product and inverse (GZKP-NTT.cu:30-48, 1725-1732).  With deg a + deg b < 2^24 the
+    cyclic product is the plain polynomial product."""
+    fid, L, log_n = 1, 4, 24
+    p, g = R.FIELDS[fid]
+    n, half = 1 << log_n, 1 << (log_n - 1)
+    pl = _plan(fid, log_n, L)
+    a = pl.fill(pl.empty(), "random", seed=5)
+    b = pl.fill(pl.empty(), "random", seed=6)
+    a[half:] = 0
+    b[half:] = 0
+    ah, bh = _host(a, L).copy(), _host(b, L).copy()
+    c = pl.empty()
+    pl.polymul(a, b, c)
+    got = _host(c, L)
+    A = OC.ntt_mp_par(ah, p, g, THREADS)
+    B = OC.ntt_mp_par(bh, p, g, THREADS)
+    exp = OC.ntt_mp_par(OC.mul_mp(A, B, p), p, g, THREADS, inverse=True)
+    assert np.array_equal(got, exp)
+    assert not got[n - 1].any()  # degree < 2^24 - 1
 
 
 C4_SEED = 4
