@@ -274,7 +274,8 @@ def main():
                                          f"{world} GPUs, one independent transform per rank (no data-path "
                                          f"collective)")),
                    "transforms_per_step": jobs,
-                   **({"exchange_pieces": len(eng.fs.pieces)} if four_step else {})},
+                   **({"exchange_pieces": len(eng.fs.pieces),
+                       "split_log_n1_n2": [eng.layout.log_n1, eng.layout.log_n2]} if four_step else {})},
     }
     # ---- SURVEY §8(d) roofline of the whole transform: 2 n S algorithmic bytes per transform
     gpus_per_transform = world if four_step else 1
