@@ -22,8 +22,11 @@
  *     status (0 ok, < 0 error, see ntt_strerror), prints nothing, and the plan API is asynchronous
  *     on the given hipStream_t (NULL = default stream).  The reference-shaped shims SSIP /
  *     NTT_GZKP_256 keep the reference's blocking behaviour.
- *   - plans are thread-compatible: one plan per thread, or serialise calls on a plan.  The status
- *     of the last call (ntt_last_error) is kept per thread; the shims' plan cache is locked.
+ *   - plans are thread-compatible: one plan per thread, or serialise calls on a plan.  A plan's
+ *     scratch is shared by its calls, so calls on one plan must also be ordered on the device (the
+ *     same stream, or streams the caller orders).  The status of the last call (ntt_last_error) is
+ *     kept per thread.  The shims are thread-safe: their plan cache is locked and each cached plan
+ *     runs one blocking call at a time.
  */
 #ifndef NTT_AMD_NTT_H
 #define NTT_AMD_NTT_H

@@ -1329,13 +1329,21 @@ int ntt_last_error(void) { return g_last_error; }
 
 // ---------------------------------------------------------------- reference-shaped shims
 // Plans are cached per (modulus, generator, limbs, log_n, device) like a persistent version of the
-// reference drivers' per-call table setup.
+// reference drivers' per-call table setup.  Threads calling a shim with the same key share the plan
+// and its scratch, so each cached plan has its own lock, held for the whole blocking call
+// (tests/test_gpu_threads.py: without it, concurrent calls overwrote each other's scratch).
+namespace {
+struct CachedPlan {
+  std::unique_ptr<ntt_plan> plan;
+  std::mutex run_mu;
+};
+}  // namespace
 static std::mutex g_cache_mu;
 static std::map<std::tuple<std::vector<uint64_t>, std::vector<uint64_t>, unsigned, unsigned, int>,
-                std::unique_ptr<ntt_plan>>
+                std::unique_ptr<CachedPlan>>
     g_cache;
 
-static ntt_plan* cached_plan(const uint64_t* p, const uint64_t* g, unsigned limbs64, unsigned log_n, int* rc) {
+static CachedPlan* cached_plan(const uint64_t* p, const uint64_t* g, unsigned limbs64, unsigned log_n, int* rc) {
   int dev = 0;
   hipGetDevice(&dev);
   auto key = std::make_tuple(std::vector<uint64_t>(p, p + limbs64), std::vector<uint64_t>(g, g + limbs64), limbs64,
@@ -1349,12 +1357,16 @@ static ntt_plan* cached_plan(const uint64_t* p, const uint64_t* g, unsigned limb
   ntt_plan* pl = nullptr;
   *rc = ntt_plan_create_custom(&pl, p, g, limbs64, log_n, dev);
   if (*rc != NTT_OK) return nullptr;
-  g_cache[key].reset(pl);
-  return pl;
+  auto& e = g_cache[key];
+  e.reset(new CachedPlan());
+  e->plan.reset(pl);
+  return e.get();
 }
 
-static int blocking_forward(ntt_plan* pl, void* d) {
-  int rc = ntt_forward(pl, d, nullptr);
+// forward on the default stream, then wait for the device, under the plan's lock
+static int blocking_forward(CachedPlan* cp, void* d) {
+  std::lock_guard<std::mutex> lk(cp->run_mu);
+  int rc = ntt_forward(cp->plan.get(), d, nullptr);
   if (rc == NTT_OK && hipDeviceSynchronize() != hipSuccess) rc = NTT_ERR_HIP;
   return set_err(rc);
 }
@@ -1362,7 +1374,7 @@ static int blocking_forward(ntt_plan* pl, void* d) {
 void SSIP(long long* x, long long omega, unsigned log_n) {
   const uint64_t p = 469762049ull, g = (uint64_t)omega;
   int rc = NTT_OK;
-  ntt_plan* pl = cached_plan(&p, &g, 1, log_n, &rc);
+  CachedPlan* pl = cached_plan(&p, &g, 1, log_n, &rc);
   if (!pl) { set_err(rc); return; }
   blocking_forward(pl, x);
 }
@@ -1373,7 +1385,7 @@ int NTT_GZKP_64(long long* data, const void* /*reverse*/, long long len, long lo
   const unsigned log_n = (unsigned)__builtin_ctzll((unsigned long long)len);
   const uint64_t p = 469762049ull, g = (uint64_t)omega;
   int rc = NTT_OK;
-  ntt_plan* pl = cached_plan(&p, &g, 1, log_n, &rc);
+  CachedPlan* pl = cached_plan(&p, &g, 1, log_n, &rc);
   if (!pl) return set_err(rc);
   return blocking_forward(pl, data);
 }
@@ -1388,7 +1400,7 @@ int NTT_GZKP_256(uint32_t* data, uint32_t len, const void* /*reverse*/, uint32_t
     g[i] = (uint64_t)omega[2 * i] | ((uint64_t)omega[2 * i + 1] << 32);
   }
   int rc = NTT_OK;
-  ntt_plan* pl = cached_plan(p, g, 4, log_n, &rc);
+  CachedPlan* pl = cached_plan(p, g, 4, log_n, &rc);
   if (!pl) return set_err(rc);
   return blocking_forward(pl, data);
 }
