@@ -299,6 +299,12 @@ enum : int { PRO_NONE = 0, PRO_PW = 1, PRO_COSET = 2 };
 // FSM: four-step addressing (PassArgs::fs) compiled in: 0 = plain batched transforms (every
 // product path), 1 = chunk maps / interleave, 2 = the same plus the output twiddle epilogue.
 // SHTW: the column pass's full outer-twiddle table holds Shoup pairs (PassArgs::tw_sh).
+// Column passes of radix < 2^NTT_COL_R32_BELOW also take the 32-bit-carry reduce_top: below radix
+// 256 they fit 122-123 VGPRs with it and no spills (radix 256 spills 28 B), -1.0 % on 2^28's four
+// radix-128 passes (profiles/r02_uni/col_r32_ab_*.txt).
+#ifndef NTT_COL_R32_BELOW
+#define NTT_COL_R32_BELOW 8
+#endif
 template <class E, int LOGR, int KIND, bool FULLTW, bool FAST, int PRO = PRO_NONE, bool SRC_USER = true,
           int FSM = 0, bool SHTW = false>
 __global__ __launch_bounds__((1 << E::TILE_LOG) / E::EPT) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
@@ -309,7 +315,8 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
   constexpr bool COLLIKE = KIND == KIND_COLUMN || KIND == KIND_STOCKHAM || KIND == KIND_DIT;  // column groups
   constexpr int TE = (KIND == KIND_SINGLE) ? (1 << LOGR) : (1 << tile_log_of<E>());
   constexpr int T = TE >> LOGR;  // columns (column pass) or blocks (final / single) per workgroup
-  constexpr bool R32 = KIND != KIND_COLUMN;  // reduce_top form (engines.hpp): column passes are at the VGPR cap
+  // reduce_top form (engines.hpp): radix-256 column passes are at the VGPR cap and keep the 64-bit one
+  constexpr bool R32 = KIND != KIND_COLUMN || LOGR < NTT_COL_R32_BELOW;
   constexpr int NT = TE / EPT;   // threads
   static_assert(LOGR >= QB && T >= 1, "radix");
   __shared__ __attribute__((aligned(16))) uint32_t lds[TE * LdsParts<E::LDSW, E::LDS_SPLIT>::max_words()];
