@@ -154,8 +154,45 @@ static int run_errors(void) {
   return 0;
 }
 
+/* `dropin bench [log_n] [steps]`: the headline transform timed from C alone (no Python): a BN254 Fr
+ * plan, vector B (seed 2) via ntt_fill, 50 warm-up forwards past the clock ramp, then `steps`
+ * forwards between two HIP events on the plan's stream.  Not part of "all". */
+static int run_bench(int argc, char** argv) {
+  const unsigned bits = argc > 2 ? (unsigned)atoi(argv[2]) : 24;
+  const int steps = argc > 3 ? atoi(argv[3]) : 100;
+  ntt_plan* plan = NULL;
+  hipStream_t s;
+  hipEvent_t e0, e1;
+  void* d = NULL;
+  int rc = ntt_plan_create(&plan, NTT_FIELD_BN254_FR, bits, 4, 0);
+  if (rc != NTT_OK) return fail("ntt_plan_create", rc);
+  HIPCHECK(hipStreamCreate(&s));
+  HIPCHECK(hipEventCreate(&e0));
+  HIPCHECK(hipEventCreate(&e1));
+  HIPCHECK(hipMalloc(&d, ((size_t)1 << bits) * 32));
+  if ((rc = ntt_fill(plan, d, 1, 2, s)) != NTT_OK) return fail("ntt_fill", rc);
+  for (int i = 0; i < 50; ++i)
+    if ((rc = ntt_forward(plan, d, s)) != NTT_OK) return fail("ntt_forward", rc);
+  HIPCHECK(hipEventRecord(e0, s));
+  for (int i = 0; i < steps; ++i)
+    if ((rc = ntt_forward(plan, d, s)) != NTT_OK) return fail("ntt_forward", rc);
+  HIPCHECK(hipEventRecord(e1, s));
+  HIPCHECK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
+  printf("BENCH_BN254 2^%u forward: %.4f ms per transform, %.4g field-elements/s (%d steps)\n", bits,
+         ms / steps, (double)((size_t)1 << bits) / (ms / steps * 1e-3), steps);
+  ntt_plan_destroy(plan);
+  HIPCHECK(hipFree(d));
+  HIPCHECK(hipEventDestroy(e0));
+  HIPCHECK(hipEventDestroy(e1));
+  HIPCHECK(hipStreamDestroy(s));
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const char* which = argc > 1 ? argv[1] : "all";
+  if (!strcmp(which, "bench")) return run_bench(argc, argv);
   int all = strcmp(which, "all") == 0;
   if ((all || !strcmp(which, "ssip")) && run_ssip()) return 1;
   if ((all || !strcmp(which, "gzkp256")) && run_gzkp256()) return 1;
