@@ -112,6 +112,26 @@ def test_mplan_polymul_matches_single_gpu(log_n, pieces):
     del mp
 
 
+def test_mplan_polymul_2pow26_chunked_rows():
+    """2^26 on the visible devices: at world size 1 the rank plan splits 2^16 x 2^10, so the row
+    transforms of a and b (nvec = 2) run in launches of 2^15 rows; bit-exact vs the one-GPU product."""
+    from ntt_amd.distributed import MultiPlan
+    fid, L, log_n = 1, 4, 26
+    exp = _single_gpu_product(fid, L, log_n, 5, 6)
+    mp = MultiPlan(fid, log_n, L, devices=list(range(torch.cuda.device_count())))
+    As = mp.fill(mp.empty(), "random", seed=5)
+    Bs = mp.fill(mp.empty(), "random", seed=6)
+    Outs = mp.empty()
+    mp.polymul(As, Bs, Outs)
+    chunk = 1 << 22  # one torch gather over 2^26 rows fails its launch configuration on this build
+    for lay, o in zip(mp.layouts, Outs):
+        idx = _row_index(lay, "cuda:0")
+        o = o.to("cuda:0")
+        for i in range(0, idx.numel(), chunk):
+            assert torch.equal(o[i:i + chunk], exp[idx[i:i + chunk]]), (lay.rank, i)
+    del mp
+
+
 def test_dist_ntt_polymul_rccl_world1():
     import torch.distributed as dist
     from ntt_amd.distributed import DistNTT
