@@ -233,6 +233,7 @@ def main():
     t1 = time.perf_counter()
     launch_avg = plan_for_prof.last_launch_ms()  # per-launch average over the timed steps (<= 64)
     plan_for_prof.set_profiling(False)
+    exchange_ms = eng.exchange_ms() if four_step else None  # mean all-to-all window per step
 
     elapsed = t1 - t0
     if use_dist:
@@ -277,6 +278,10 @@ def main():
                    **({"exchange_pieces": len(eng.fs.pieces),
                        "split_log_n1_n2": [eng.layout.log_n1, eng.layout.log_n2]} if four_step else {})},
     }
+    if four_step:
+        # rank 0's all-to-all window per transform (HIP events on the compute stream around the
+        # exchange: from the first piece's start to the last piece's arrival)
+        out["exchange_ms"] = exchange_ms
     # ---- SURVEY §8(d) roofline of the whole transform: 2 n S algorithmic bytes per transform
     gpus_per_transform = world if four_step else 1
     alg_transform = 2 * n * elem_bytes

@@ -300,6 +300,11 @@ class DistNTT:
         self.fs = FourStep(self.layout, self.engine, self, pieces=pieces)
         self.n = self.layout.n
         self.passes: List[int] = []  # per-transform schedules: see the row / column plans
+        # exchange timing (set_profiling): one window per all-to-all, from the first piece's start to
+        # the last piece's arrival, as HIP events on the compute stream (so a window that overlaps
+        # row transforms of later pieces includes them)
+        self._x_windows: Optional[list] = None
+        self._x_open: Optional[list] = None
 
     # RCCL moves < 2 GiB per peer per collective (a 2 GiB chunk arrived half copied,
     # tests/test_gpu_fullsize.py): larger per-peer runs go as several all-to-alls.
@@ -308,6 +313,12 @@ class DistNTT:
     # ---- FourStep exchange interface: rows [row0, row0 + nrows) of every peer chunk
     def start(self, send, recv, nvec, row0, nrows):
         L = self.layout
+        if self._x_windows is not None and (self._x_open is None or self._x_open[1] is not None):
+            if self._x_open is not None:
+                self._x_windows.append(self._x_open)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            self._x_open = [e0, None]
         sv = piece_views(send, L.world, nvec, L.r, L.c, row0, nrows)
         rv = piece_views(recv, L.world, nvec, L.r, L.c, row0, nrows)
         works = []
@@ -331,6 +342,19 @@ class DistNTT:
     def wait(self, works):
         for w in works:
             w.wait()
+        if self._x_windows is not None and self._x_open is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self._x_open[1] = e1
+
+    def exchange_ms(self) -> Optional[float]:
+        """Mean all-to-all window (ms) over the exchanges since set_profiling(True)."""
+        done = self._x_windows if self._x_windows is not None else getattr(self, "_x_frozen", [])
+        wins = list(done) + ([self._x_open] if self._x_open and self._x_open[1] else [])
+        if not wins:
+            return None
+        torch.cuda.synchronize()
+        return sum(a.elapsed_time(b) for a, b in wins) / len(wins)
 
     def empty(self) -> torch.Tensor:
         return self.engine.empty(self.layout.local_n)
@@ -350,7 +374,17 @@ class DistNTT:
         return self.fs.polymul(a, b, out)
 
     def set_profiling(self, enable: bool = True) -> None:
+        """Per-launch timing of the rank plan and, from here on, exchange windows (exchange_ms);
+        disabling stops recording but keeps what was measured."""
         self.engine.set_profiling(enable)
+        if enable:
+            self._x_windows, self._x_open = [], None
+        elif self._x_windows is not None:
+            if self._x_open is not None and self._x_open[1] is not None:
+                self._x_windows.append(self._x_open)
+            self._x_open = None
+            self._x_frozen = self._x_windows
+            self._x_windows = None
 
     def last_launch_ms(self) -> List[float]:
         """Row-transform launches, then column-transform launches (separate timing rings)."""
