@@ -84,6 +84,17 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
  * default schedule; P469762049 (1 limb) and 4-limb plans, single transforms (batch 1).
  * NTT_PLAN_STOCKHAM and NTT_PLAN_GZKP are exclusive. */
 #define NTT_PLAN_GZKP 8u
+/* In place, no scratch (the reference's self-sort-in-place property, SSIP_NTT_stage2's mirror pairs,
+ * GZKP-NTT.cu:1359-1449): the plan owns no n-element buffer.  The radices are arranged as a
+ * palindrome (R_1 = R_p, middle radices symmetric; one pass more than the default schedule when
+ * log_n admits no palindrome of that length, e.g. odd log_n over an even pass count), every pass
+ * writes the positions it read, and the digit reversal is a final pass of disjoint tile-pair swaps
+ * (the permutation is an involution).  Same contract and results as the default schedule; one more
+ * read + write of the vector.  Plans whose scratch element is narrower than the caller's (the
+ * 6-limb 256-bit layout, the 8-B P path with its 4-B scratch), sizes with no palindrome the pass
+ * kernels accept (2^11 and 2^13 on the 1024-element tiles) and the rival schedules return
+ * NTT_ERR_ARG. */
+#define NTT_PLAN_IN_PLACE 16u
 int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags);
 
 /* Modulus-generic plan, like big-num.cu's `prime` / `omega` kernel arguments (big-num.cu:68,173,260):

@@ -61,7 +61,8 @@ struct PassArgs {
   uint32_t nmid;     // final pass: number of middle digits (p - 2)
   uint32_t mid_bits[4];  // final pass: middle digit widths, least significant (k_{p-1}) first
   uint32_t mid_off[4];   // final pass: output bit offset (relative to R_1) of those digits
-  uint32_t flags;        // bit 0: multiply outputs by ninv (single-pass inverse)
+  uint32_t flags;        // bit 0: multiply outputs by ninv (single-pass inverse); bit 1: final pass
+                         // writes each output to its input's position (NTT_PLAN_IN_PLACE)
   uint32_t src_user;     // column pass: src is the caller's buffer (E::MEMW words/element), not scratch (E::SCRW)
   size_t batch_stride;   // 32-bit words between batched transforms in the caller's buffers (n * E::MEMW)
   // ---- distributed four-step addressing (ntt_rplan_*); fs == 0: plain batched transforms.
@@ -122,6 +123,16 @@ hipError_t launch_twiddle_pack(const uint32_t* src, uint32_t* dst, uint32_t log_
 template <class E>
 hipError_t launch_transpose(const uint32_t* src, uint32_t* dst, uint32_t log_rows, uint32_t log_cols,
                             uint32_t log_blk_rows, uint64_t blk_stride, hipStream_t st);
+// In-place digit reversal of a palindromic schedule (NTT_PLAN_IN_PLACE): position
+// (k1, mid, kn) = k1 2^(log_n - R) + mid 2^R + kn  <->  (kn, midrev, k1), tiles of 2^tb_log x 2^tb_log.
+struct DrevArgs {
+  uint32_t log_n, R, tb_log, nmid;
+  uint32_t mid_bits[4];  // middle digit widths of `mid`, least significant first (PassArgs::mid_bits)
+  uint32_t mid_off[4];   // their bit offsets in midrev (PassArgs::mid_off)
+  size_t batch_stride;   // 32-bit words between batched transforms
+};
+template <class E>
+hipError_t launch_digitrev_swap(uint32_t* data, const DrevArgs& A, uint32_t batch, hipStream_t st);
 // data[j] *= c^j (coset / low-degree-extension scale), c^j = lo_s[j & mask] * hi[j >> lo_bits]
 template <class E>
 hipError_t launch_scale_pow(uint32_t* data, uint32_t log_n, uint32_t batch, const uint32_t* lo_s, const uint32_t* hi,

@@ -560,6 +560,8 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
           if (fs_il) {
             const uint32_t k1 = k10 + (c >> tb_log), b = b0 + (c & ((1u << tb_log) - 1));
             pos = (((size_t)k1 + ((size_t)midrev << A.r1) + ((size_t)kn << (A.log_n - LOGR))) << A.il) + b;
+          } else if (A.flags & 2u) {  // NTT_PLAN_IN_PLACE: the input's own position; k_digitrev_swap follows
+            pos = ((size_t)(k10 + c) << (A.log_n - A.r1)) + ((size_t)mid << LOGR) + kn;
           } else {
             pos = (size_t)(k10 + c) + ((size_t)midrev << A.r1) + ((size_t)kn << (A.log_n - LOGR));
           }
@@ -911,6 +913,84 @@ hipError_t launch_transpose(const uint32_t* src, uint32_t* dst, uint32_t log_row
   return hipGetLastError();
 }
 
+// In-place digit reversal after an in-place final pass (NTT_PLAN_IN_PLACE; the replacement for the
+// reference's SSIP stage-2 mirror pairs, GZKP-NTT.cu:1359-1449).  With a palindromic radix sequence
+// (R_1 = R_p = 2^R, middle widths symmetric) the element at position (k1, mid, kn) =
+// k1 2^(L-R) + mid 2^R + kn belongs at (kn, midrev, k1): an involution, so the permutation is a set of
+// disjoint swaps.  A workgroup owns the tile pair {(I tb + a, mid, J tb + b)} and its image
+// {(J tb + a, midrev, I tb + b)} (a, b < tb): both tiles are read as tb-element contiguous rows, swapped
+// through LDS and written back transposed.  Of the two workgroups of a pair the one with the larger
+// index exits; a tile that is its own image (mid = midrev, I = J) is transposed in place.
+template <int MW>
+__global__ __launch_bounds__(256) void k_digitrev_swap(uint32_t* data, DrevArgs A) {
+  constexpr int SL = MW + 1;  // LDS slot stride (words): odd, so transposed reads spread over banks
+  __shared__ uint32_t tile[2][256 * SL];
+  const uint32_t tl = A.tb_log, ntl = A.R - tl;
+  const uint64_t u = blockIdx.x;
+  const uint32_t J = (uint32_t)(u & ((1u << ntl) - 1)), I = (uint32_t)((u >> ntl) & ((1u << ntl) - 1));
+  const uint64_t mid = u >> (2 * ntl);
+  uint64_t m = mid, midrev = 0;
+  for (uint32_t i = 0; i < A.nmid; ++i) {
+    midrev |= (m & ((1ull << A.mid_bits[i]) - 1)) << A.mid_off[i];
+    m >>= A.mid_bits[i];
+  }
+  const uint64_t partner = (midrev << (2 * ntl)) | ((uint64_t)J << ntl) | I;
+  if (partner < u) return;  // the pair is handled by the partner's workgroup (uniform exit)
+  uint32_t* d = data + (size_t)blockIdx.y * A.batch_stride;
+  const uint32_t t = threadIdx.x, tb = 1u << tl;
+  const bool act = t < (tb << tl);
+  const uint32_t a = t >> tl, b = t & (tb - 1);
+  const uint32_t sh = A.log_n - A.R;
+  const size_t posA = ((size_t)(I * tb + a) << sh) + (mid << A.R) + J * tb + b;
+  const size_t posB = ((size_t)(J * tb + a) << sh) + (midrev << A.R) + I * tb + b;
+  uint32_t va[MW], vb[MW];
+  if (act) {
+    if constexpr (MW % 4 == 0) {
+#pragma unroll
+      for (int w = 0; w < MW / 4; ++w) {
+        const uint4 x = reinterpret_cast<const uint4*>(d + posA * MW)[w];
+        const uint4 y = reinterpret_cast<const uint4*>(d + posB * MW)[w];
+        va[4 * w] = x.x, va[4 * w + 1] = x.y, va[4 * w + 2] = x.z, va[4 * w + 3] = x.w;
+        vb[4 * w] = y.x, vb[4 * w + 1] = y.y, vb[4 * w + 2] = y.z, vb[4 * w + 3] = y.w;
+      }
+    } else {
+#pragma unroll
+      for (int w = 0; w < MW; ++w) va[w] = d[posA * MW + w], vb[w] = d[posB * MW + w];
+    }
+#pragma unroll
+    for (int w = 0; w < MW; ++w) tile[0][t * SL + w] = va[w], tile[1][t * SL + w] = vb[w];
+  }
+  __syncthreads();
+  if (!act) return;
+  const uint32_t tt = (b << tl) + a;  // the transposed slot
+#pragma unroll
+  for (int w = 0; w < MW; ++w) va[w] = tile[1][tt * SL + w], vb[w] = tile[0][tt * SL + w];
+  const bool self = partner == u;
+  if constexpr (MW % 4 == 0) {
+#pragma unroll
+    for (int w = 0; w < MW / 4; ++w) {
+      reinterpret_cast<uint4*>(d + posA * MW)[w] = make_uint4(va[4 * w], va[4 * w + 1], va[4 * w + 2], va[4 * w + 3]);
+      if (!self)
+        reinterpret_cast<uint4*>(d + posB * MW)[w] = make_uint4(vb[4 * w], vb[4 * w + 1], vb[4 * w + 2], vb[4 * w + 3]);
+    }
+  } else {
+#pragma unroll
+    for (int w = 0; w < MW; ++w) {
+      d[posA * MW + w] = va[w];
+      if (!self) d[posB * MW + w] = vb[w];
+    }
+  }
+}
+
+template <class E>
+hipError_t launch_digitrev_swap(uint32_t* data, const DrevArgs& A, uint32_t batch, hipStream_t st) {
+  if (A.R < A.tb_log || 2 * A.R > A.log_n || A.tb_log > 4) return hipErrorInvalidValue;
+  const uint64_t units = 1ull << (A.log_n - 2 * A.tb_log);
+  if (units > 0xffffffffull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((k_digitrev_swap<E::MEMW>), dim3((uint32_t)units, batch), dim3(256), 0, st, data, A);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------- utility kernels
 __device__ __forceinline__ uint64_t splitmix64(uint64_t c) {
   uint64_t z = c + 0x9E3779B97F4A7C15ull;
@@ -1185,6 +1265,7 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
                                              const typename E::Args&, uint64_t, hipStream_t);                      \
   template hipError_t launch_transpose<E>(const uint32_t*, uint32_t*, uint32_t, uint32_t, uint32_t, uint64_t,     \
                                           hipStream_t);                                                            \
+  template hipError_t launch_digitrev_swap<E>(uint32_t*, const DrevArgs&, uint32_t, hipStream_t);                  \
   template hipError_t launch_pointwise<E>(const uint32_t*, const uint32_t*, uint32_t*, size_t,                     \
                                           const typename E::Args&, const uint32_t*, hipStream_t);                  \
   template hipError_t launch_build_tw<E>(uint32_t*, size_t, uint32_t, uint32_t, uint32_t, const uint32_t*,        \

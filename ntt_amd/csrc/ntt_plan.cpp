@@ -165,6 +165,46 @@ static bool schedule(unsigned log_n, unsigned tile_log, unsigned min_cols_log, b
   return schedule_ok(r, p, tile_log);
 }
 
+// NTT_PLAN_IN_PLACE: a palindromic sequence (r_i = r_{p-1-i}, 3 <= r_i <= rmax, schedule_ok) with the
+// fewest passes (>= p0), then the smallest largest radix, then the largest smallest one.  The digit
+// reversal of a palindromic sequence is an involution (k_digitrev_swap).
+static bool schedule_palindrome(unsigned log_n, unsigned tile_log, unsigned rmax, unsigned p0, unsigned* r,
+                                unsigned& p) {
+  if (rmax < 3) return false;
+  const unsigned span = rmax - 2;  // radices 3..rmax
+  for (unsigned pp = (p0 < 2 ? 2 : p0); pp <= 8; ++pp) {
+    const unsigned h = (pp + 1) / 2;
+    unsigned combos = 1;
+    for (unsigned i = 0; i < h; ++i) combos *= span;
+    unsigned best[8] = {0}, bmax = 99, bmin = 0;
+    for (unsigned code = 0; code < combos; ++code) {
+      unsigned v[8], c = code, sum = 0, mx = 0, mn = 99;
+      for (unsigned i = 0; i < h; ++i) {
+        v[i] = 3 + c % span;
+        c /= span;
+      }
+      for (unsigned i = 0; i < pp; ++i) {
+        v[i] = v[i < h ? i : pp - 1 - i];
+        sum += v[i];
+        mx = v[i] > mx ? v[i] : mx;
+        mn = v[i] < mn ? v[i] : mn;
+      }
+      if (sum != log_n || !schedule_ok(v, pp, tile_log)) continue;
+      if (mx < bmax || (mx == bmax && mn > bmin)) {
+        bmax = mx;
+        bmin = mn;
+        for (unsigned i = 0; i < pp; ++i) best[i] = v[i];
+      }
+    }
+    if (bmax != 99) {
+      p = pp;
+      for (unsigned i = 0; i < pp; ++i) r[i] = best[i];
+      return true;
+    }
+  }
+  return false;
+}
+
 // ------------------------------------------------------------------------------ engine encodings
 // The host does all table arithmetic in 32-bit Montgomery form (HostField<NH>), produces canonical
 // values, then encodes them in the engine's own Montgomery domain / limb layout.
@@ -432,6 +472,14 @@ struct PlanImpl final : PlanBase {
     // ---- schedule + tables (engine-encoded)
     if (!schedule(log_n, tile_log_of<E>(), E::MIN_COLS_LOG, !E::PASS1_FULL_TABLE && NTT_P_NARROW_FIRST, r, npass))
       return NTT_ERR_ARG;
+    if (flags & NTT_PLAN_IN_PLACE) {
+      // passes store their lazily reduced values where they read them: the scratch element must be
+      // the caller's element
+      if (E::SCRW != E::MEMW) return NTT_ERR_ARG;
+      if (npass >= 2 &&
+          !schedule_palindrome(log_n, tile_log_of<E>(), tile_log_of<E>() - E::MIN_COLS_LOG, npass, r, npass))
+        return NTT_ERR_ARG;
+    }
     const bool twiddle_only = (flags & NTT_PLAN_TWIDDLE_ONLY) != 0;
     std::vector<uint32_t> host;
     auto push_powers = [&](const Vec<NH>& base_m, uint64_t count, const Vec<NH>* scale_m,
@@ -499,7 +547,7 @@ struct PlanImpl final : PlanBase {
     if (hipMalloc(&d_tab, host.size() * 4) != hipSuccess ||
         hipMemcpy(d_tab, host.data(), host.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
       rc = NTT_ERR_HIP;
-    if (rc == NTT_OK && npass >= 2 && !twiddle_only) rc = ensure_scratch(1);
+    if (rc == NTT_OK && npass >= 2 && !twiddle_only && !(flags & NTT_PLAN_IN_PLACE)) rc = ensure_scratch(1);
     if (rc == NTT_OK && npass >= 2 && !twiddle_only) rc = build_full_tables();
     // NTT_PLAN_GZKP runs on the same per-pass tables: Stockham pass i's w_n^((k pi) << (log_n - lgp_i - r_i))
     // for k < 2^lgp_i is the GZKP DIT pass's w_N^(c d), N = 2^(lgp_i + r_i)
@@ -896,7 +944,14 @@ struct PlanImpl final : PlanBase {
       mark(st);
     } else {
       if (il) batch = 1;  // Mode I: the 2^il interleaved transforms are one long column sweep
-      if (int rc = ensure_scratch(il ? (1u << il) : batch)) return rc;
+      // NTT_PLAN_IN_PLACE (not for four-step pieces, whose passes map positions): every pass reads and
+      // writes `out`'s positions, the final pass included; the digit reversal follows as tile swaps
+      const bool inplace = (flags & NTT_PLAN_IN_PLACE) && !io;
+      uint32_t* work = inplace ? out : d_scratch;
+      if (!inplace) {
+        if (int rc = ensure_scratch(il ? (1u << il) : batch)) return rc;
+        work = d_scratch;
+      }
       const uint32_t grid = (uint32_t)((n << il) >> tile_log_of<E>());
       unsigned blk = log_n;
       for (unsigned i = 0; i + 1 < npass && e == hipSuccess; ++i) {
@@ -923,8 +978,8 @@ struct PlanImpl final : PlanBase {
         A.log_m = log_n - blk;
         A.src_user = (i == 0) ? 1u : 0u;
         set_fs(A, i == 0 ? FS_MAP_IN : 0u);
-        const uint32_t* src = (i == 0) ? in : d_scratch;
-        e = launch_pass<E>(KIND_COLUMN, (int)r[i], src, d_scratch, A, grid, batch, st);
+        const uint32_t* src = (i == 0) ? in : work;
+        e = launch_pass<E>(KIND_COLUMN, (int)r[i], src, work, A, grid, batch, st);
         mark(st);
         blk -= r[i];
       }
@@ -943,8 +998,20 @@ struct PlanImpl final : PlanBase {
         }
         set_fs(A, FS_MAP_OUT);
         if (io) A.tw_epi = static_cast<const uint32_t*>(io->tw_epi);
-        e = launch_pass<E>(KIND_FINAL, (int)r[npass - 1], d_scratch, out, A, grid, batch, st);
+        if (inplace) A.flags |= 2u;
+        e = launch_pass<E>(KIND_FINAL, (int)r[npass - 1], work, out, A, grid, batch, st);
         mark(st);
+        if (inplace && e == hipSuccess) {
+          DrevArgs D{};
+          D.log_n = log_n;
+          D.R = r[0];
+          D.tb_log = r[0] < 4 ? r[0] : 4;
+          D.nmid = A.nmid;
+          for (unsigned m = 0; m < A.nmid; ++m) D.mid_bits[m] = A.mid_bits[m], D.mid_off[m] = A.mid_off[m];
+          D.batch_stride = (size_t)n * MEMW;
+          e = launch_digitrev_swap<E>(out, D, batch, st);
+          mark(st);
+        }
       }
     }
     return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
@@ -1087,6 +1154,8 @@ static int make_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, const 
   if (log_n > 40) return NTT_ERR_ARG;
   if (limbs64 != 1 && limbs64 != 4 && limbs64 != 6) return NTT_ERR_ARG;  // before packing into p32[12] / g32[12]
   if ((flags & NTT_PLAN_STOCKHAM) && (flags & NTT_PLAN_GZKP)) return NTT_ERR_ARG;  // one rival schedule per plan
+  if ((flags & NTT_PLAN_IN_PLACE) && (flags & (NTT_PLAN_STOCKHAM | NTT_PLAN_GZKP | NTT_PLAN_TWIDDLE_ONLY)))
+    return NTT_ERR_ARG;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return NTT_ERR_NODEV;
   if (device < 0 || device >= ndev) return NTT_ERR_ARG;

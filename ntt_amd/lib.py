@@ -21,6 +21,7 @@ NTT_PLAN_TWIDDLE_ONLY = 1
 NTT_PLAN_MONTGOMERY_IO = 2
 NTT_PLAN_STOCKHAM = 4
 NTT_PLAN_GZKP = 8
+NTT_PLAN_IN_PLACE = 16
 
 # Every symbol declared in include/ntt.h with its ctypes prototype: (restype, argtypes).
 _vp = C.c_void_p

@@ -85,6 +85,14 @@ def main():
          passes=pl.passes)
     del pl, t
     torch.cuda.empty_cache()
+    # NTT_PLAN_IN_PLACE (no plan scratch): palindromic passes + the tile-swap digit reversal
+    for lg, (w, s) in ((24, (30, 20)), (28, (3, 5))):
+        pl = NTTPlan(1, lg, 4, in_place=True)
+        t = pl.fill(pl.empty(), "random", seed=4)
+        emit(f"in place: 2^{lg} forward BN254 Fr (NTT_PLAN_IN_PLACE, no scratch)", 1 << lg,
+             timeit(lambda: pl.forward(t), w, s), passes=pl.passes)
+        del pl, t
+        torch.cuda.empty_cache()
     for pieces in (1, 4):
         vr = VirtualRanks(1, 28, 4, 8, pieces=pieces)
         xs = vr.fill(vr.empty(), "random", seed=4)
