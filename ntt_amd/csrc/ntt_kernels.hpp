@@ -127,6 +127,7 @@ hipError_t launch_transpose(const uint32_t* src, uint32_t* dst, uint32_t log_row
 // (k1, mid, kn) = k1 2^(log_n - R) + mid 2^R + kn  <->  (kn, midrev, k1), tiles of 2^tb_log x 2^tb_log.
 struct DrevArgs {
   uint32_t log_n, R, tb_log, nmid;
+  uint32_t diag;         // workgroup -> tile-pair order: 1 diagonal, 0 row-major
   uint32_t mid_bits[4];  // middle digit widths of `mid`, least significant first (PassArgs::mid_bits)
   uint32_t mid_off[4];   // their bit offsets in midrev (PassArgs::mid_off)
   size_t batch_stride;   // 32-bit words between batched transforms

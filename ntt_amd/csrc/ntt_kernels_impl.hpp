@@ -927,14 +927,21 @@ __global__ __launch_bounds__(256) void k_digitrev_swap(uint32_t* data, DrevArgs 
   __shared__ uint32_t tile[2][256 * SL];
   const uint32_t tl = A.tb_log, ntl = A.R - tl;
   const uint64_t u = blockIdx.x;
-  const uint32_t J = (uint32_t)(u & ((1u << ntl) - 1)), I = (uint32_t)((u >> ntl) & ((1u << ntl) - 1));
+  const uint32_t nm = (1u << ntl) - 1;
+  const uint32_t lo = (uint32_t)(u & nm), hi = (uint32_t)((u >> ntl) & nm);
+  // diagonal order (A.diag): I = lo, J = lo + hi, so that neighbouring workgroups differ in both tile
+  // coordinates and neither tile of a pair walks down one column of 2^(log_n - R)-element rows
+  // (power-of-two strides that land on the same HBM channels); else row-major (I = hi, J = lo)
+  const uint32_t I = A.diag ? lo : hi, J = A.diag ? ((lo + hi) & nm) : lo;
   const uint64_t mid = u >> (2 * ntl);
   uint64_t m = mid, midrev = 0;
   for (uint32_t i = 0; i < A.nmid; ++i) {
     midrev |= (m & ((1ull << A.mid_bits[i]) - 1)) << A.mid_off[i];
     m >>= A.mid_bits[i];
   }
-  const uint64_t partner = (midrev << (2 * ntl)) | ((uint64_t)J << ntl) | I;
+  // the image tile (midrev, J, I) in the same order
+  const uint64_t partner = (midrev << (2 * ntl)) |
+                           (A.diag ? (((uint64_t)((I - J) & nm) << ntl) | J) : (((uint64_t)J << ntl) | I));
   if (partner < u) return;  // the pair is handled by the partner's workgroup (uniform exit)
   uint32_t* d = data + (size_t)blockIdx.y * A.batch_stride;
   const uint32_t t = threadIdx.x, tb = 1u << tl;

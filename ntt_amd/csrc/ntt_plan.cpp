@@ -1009,6 +1009,11 @@ struct PlanImpl final : PlanBase {
           D.nmid = A.nmid;
           for (unsigned m = 0; m < A.nmid; ++m) D.mid_bits[m] = A.mid_bits[m], D.mid_off[m] = A.mid_off[m];
           D.batch_stride = (size_t)n * MEMW;
+          static const int drev_diag = [] {
+            const char* v = getenv("NTT_DREV_DIAG");
+            return v ? atoi(v) : 1;
+          }();
+          D.diag = drev_diag ? 1u : 0u;
           e = launch_digitrev_swap<E>(out, D, batch, st);
           mark(st);
         }
