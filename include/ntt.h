@@ -90,10 +90,10 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
  * log_n admits no palindrome of that length, e.g. odd log_n over an even pass count), every pass
  * writes the positions it read, and the digit reversal is a final pass of disjoint tile-pair swaps
  * (the permutation is an involution).  Same contract and results as the default schedule; one more
- * read + write of the vector.  Plans whose scratch element is narrower than the caller's (the
- * 6-limb 256-bit layout, the 8-B P path with its 4-B scratch), sizes with no palindrome the pass
- * kernels accept (2^11 and 2^13 on the 1024-element tiles) and the rival schedules return
- * NTT_ERR_ARG. */
+ * read + write of the vector.  P469762049 plans run on 8-B scratch elements for it (the default P
+ * plan keeps 4-B ones).  The 6-limb 256-bit layout (48-B elements, 32-B scratch), sizes with no
+ * palindrome the pass kernels accept (2^11 and 2^13 on the 1024-element tiles; P: 2^15, 2^17, 2^19
+ * on its 8192-element tiles) and the rival schedules return NTT_ERR_ARG. */
 #define NTT_PLAN_IN_PLACE 16u
 int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags);
 

@@ -289,13 +289,14 @@ struct Eng29 {
 // N x 32-bit limbs, canonical residues, CIOS/FIPS Montgomery (field.hpp).  Used for the 1-limb
 // P469762049 `long long` path (MEMW = 2).  Twiddles are stored in Montgomery form (w R), so
 // mont_mul(x, w R) = x w; every value stays canonical and the lazy-bound parameters are ignored.
-template <int N, int MEMW_>
+template <int N, int MEMW_, int SCR_ = 0>
 struct Eng32 {
   static constexpr int W = N;
   static constexpr int MEMW = MEMW_;
   // 1-limb P path: values < 2^31, so the plan's scratch and tables hold 4 B per element where the
-  // caller's `long long` layout holds 8 (HBM-bound path: a third less traffic per transform)
-  static constexpr int SCRW = (N == 1 && NTT_P_SCRATCH32) ? 1 : MEMW_;
+  // caller's `long long` layout holds 8 (HBM-bound path: a third less traffic per transform).
+  // SCR_ != 0 forces the scratch width (EngPI: the caller's 8 B, for NTT_PLAN_IN_PLACE)
+  static constexpr int SCRW = SCR_ ? SCR_ : ((N == 1 && NTT_P_SCRATCH32) ? 1 : MEMW_);
   static constexpr int TW = N;
   static constexpr int LDSW = N;
   static constexpr int IN = 4;

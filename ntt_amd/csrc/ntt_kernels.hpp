@@ -1,5 +1,6 @@
 // Kernel-facing argument structs and launcher declarations (host + device).
 #pragma once
+#include <type_traits>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "engines.hpp"
@@ -26,6 +27,11 @@ using Eng256 = Eng29<9, 8>;    // 4 x 64-bit limbs in HBM
 using Eng384 = Eng29<14, 12>;  // 6 x 64-bit limbs in HBM, moduli up to 2^383
 using Eng256w = Eng29<9, 12>;  // 6 x 64-bit limbs in HBM, moduli < 2^255 (256-bit arithmetic)
 using EngP = Eng32<1, 2>;      // P469762049, `long long` in HBM
+using EngPI = Eng32<1, 2, 2>;  // the same with 8-B scratch elements: NTT_PLAN_IN_PLACE plans of P
+template <class E>
+struct IsEng32 : std::false_type {};
+template <int N, int M, int S>
+struct IsEng32<Eng32<N, M, S>> : std::true_type {};
 template <>
 struct HasStockham<Eng256> {
   static constexpr bool value = true;

@@ -304,10 +304,10 @@ struct EngHost<Eng29<L, W32>> {
   }
 };
 
-template <int N, int MEMW_>
-struct EngHost<Eng32<N, MEMW_>> {
+template <int N, int MEMW_, int SCR_>
+struct EngHost<Eng32<N, MEMW_, SCR_>> {
   static constexpr int NH = N;
-  using EA = typename Eng32<N, MEMW_>::Args;
+  using EA = typename Eng32<N, MEMW_, SCR_>::Args;
   HostField<NH> const* H = nullptr;
   void init(const HostField<NH>& h) { H = &h; }
   void encode(const Vec<NH>& c, uint32_t* out) const {
@@ -862,7 +862,7 @@ struct PlanImpl final : PlanBase {
 
   // canonical value of the engine's Montgomery radix R_e mod p
   Vec<NH> engine_radix_mod_p() const {
-    if constexpr (std::is_same<E, Eng32<E::W, E::MEMW>>::value) {
+    if constexpr (IsEng32<E>::value) {
       return H.r1;  // 2^(32N) mod p
     } else {
       return EH.kR;  // 2^(29L) mod p
@@ -1174,9 +1174,15 @@ static int make_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, const 
   int rc;
   if (limbs64 == 1) {
     if (p64[0] >= (1ull << 31)) return NTT_ERR_FIELD;  // `long long` path: 31-bit primes
-    auto impl = std::make_unique<PlanImpl<EngP>>();
-    rc = impl->init(p32, g32, log_n, device, flags);
-    out = std::move(impl);
+    if (flags & NTT_PLAN_IN_PLACE) {  // in place needs 8-B scratch elements (the caller's layout)
+      auto impl = std::make_unique<PlanImpl<EngPI>>();
+      rc = impl->init(p32, g32, log_n, device, flags);
+      out = std::move(impl);
+    } else {
+      auto impl = std::make_unique<PlanImpl<EngP>>();
+      rc = impl->init(p32, g32, log_n, device, flags);
+      out = std::move(impl);
+    }
   } else if (limbs64 == 4) {
     auto impl = std::make_unique<PlanImpl<Eng256>>();
     rc = impl->init(p32, g32, log_n, device, flags);

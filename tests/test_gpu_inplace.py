@@ -162,7 +162,39 @@ def test_in_place_384bit_class():
         assert np.array_equal(_host(t, 6), x), log_n
 
 
-@pytest.mark.parametrize("kw", [dict(fid=0, log_n=16, L=1),            # P: 4-B scratch, 8-B elements
+GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "ref_p469762049.npz"))
+
+
+@pytest.mark.parametrize("log_n", [14, 16, 18, 20, 21, 22, 24, 26])
+def test_in_place_p_path_vs_reference_outputs(log_n):
+    """The reference's own field and SSIP contract (`long long` elements, P = 469762049, x_j = j and a
+    seeded vector): sampled outputs of the reference's CPU NTT (tests/golden/ref_p469762049.npz),
+    bit-for-bit agreement with the default schedule, round trip.  P plans with NTT_PLAN_IN_PLACE run
+    on 8-B scratch elements (EngPI) and the 8192-element tiles (palindromes with r_1 + r_p >= 13)."""
+    n = 1 << log_n
+    ip = _plan(0, log_n, 1)
+    assert _is_palindrome(ip.passes) and sum(ip.passes) == log_n, ip.passes
+    idx = torch.from_numpy(GOLD[f"samp_idx_{log_n}"]).to("cuda:0") if f"samp_idx_{log_n}" in GOLD else None
+    t = torch.arange(n, dtype=torch.int64, device="cuda:0")
+    ip.forward(t)
+    if idx is not None:
+        assert np.array_equal(t[idx].cpu().numpy(), GOLD[f"samp_iota_{log_n}"])
+    x = OC.random_limbs(0, n, seed=2000 + log_n, L=1)[:, 0].astype(np.int64)
+    a = torch.from_numpy(x).to("cuda:0")
+    b = a.clone()
+    ip.forward(a)
+    _plan(0, log_n, 1, in_place=False).forward(b)
+    assert torch.equal(a, b)
+    if idx is not None:
+        assert np.array_equal(a[idx].cpu().numpy(), GOLD[f"samp_rand_{log_n}"])
+    if log_n <= 16:
+        p, g = R.FIELDS[0]
+        assert np.array_equal(a.cpu().numpy(), OC.ntt_u64(x, p, g))
+    ip.inverse(a)
+    assert np.array_equal(a.cpu().numpy(), x)
+
+
+@pytest.mark.parametrize("kw", [dict(fid=0, log_n=15, L=1),            # P: no palindrome with r_1 + r_p >= 13
                                 dict(fid=1, log_n=16, L=6),            # 6-limb 256-bit: 32-B scratch, 48-B elements
                                 dict(fid=1, log_n=11, L=4),            # no palindrome with r_1 + r_p >= 10
                                 dict(fid=1, log_n=13, L=4),            # ... and r_{p-1} + r_p >= 10
