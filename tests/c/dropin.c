@@ -61,6 +61,33 @@ static int run_ssip(void) {
   return 0;
 }
 
+/* The SSIP call site with no plan scratch (NTT_PLAN_IN_PLACE): the reference's self-sort-in-place
+ * property kept (GZKP-NTT.cu:1359-1449), n = 2^26, x_j = j, the same outputs as SSIP. */
+static int run_inplace(void) {
+  const unsigned bits = 26;
+  const size_t n = (size_t)1 << bits;
+  ntt_plan* plan = NULL;
+  int rc = ntt_plan_create_ex(&plan, NTT_FIELD_P469762049, bits, 1, 0, NTT_PLAN_IN_PLACE);
+  if (rc != NTT_OK) return fail("ntt_plan_create_ex(NTT_PLAN_IN_PLACE)", rc);
+  long long* h = (long long*)malloc(n * sizeof(long long));
+  long long* d = NULL;
+  for (size_t i = 0; i < n; ++i) h[i] = (long long)i;
+  HIPCHECK(hipMalloc((void**)&d, n * sizeof(long long)));
+  HIPCHECK(hipMemcpy(d, h, n * sizeof(long long), hipMemcpyHostToDevice));
+  if ((rc = ntt_forward(plan, d, NULL)) != NTT_OK) return fail("ntt_forward (in place)", rc);
+  HIPCHECK(hipMemcpy(h, d, n * sizeof(long long), hipMemcpyDeviceToHost));
+  print_samples("INPLACE_SSIP", bits, h, 1);
+  if ((rc = ntt_inverse(plan, d, NULL)) != NTT_OK) return fail("ntt_inverse (in place)", rc);
+  HIPCHECK(hipMemcpy(h, d, n * sizeof(long long), hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < n; ++i)
+    if (h[i] != (long long)i) return fail("in-place inverse round trip", -102);
+  printf("INPLACE_ROUNDTRIP %u ok\n", bits);
+  ntt_plan_destroy(plan);
+  HIPCHECK(hipFree(d));
+  free(h);
+  return 0;
+}
+
 /* NTT_GZKP<8,256>: big-num.cu main, n = 2^5 .. 2^12, cgbn_mem_t<256> (8 x u32 LE) elements */
 static int run_gzkp256(void) {
   uint32_t prime[8] = {0}, omega[8] = {0};
@@ -198,6 +225,7 @@ int main(int argc, char** argv) {
   if ((all || !strcmp(which, "gzkp256")) && run_gzkp256()) return 1;
   if ((all || !strcmp(which, "gzkp64")) && run_gzkp64()) return 1;
   if ((all || !strcmp(which, "plan")) && run_plan()) return 1;
+  if ((all || !strcmp(which, "inplace")) && run_inplace()) return 1;
   if ((all || !strcmp(which, "errors")) && run_errors()) return 1;
   printf("DONE\n");
   return 0;

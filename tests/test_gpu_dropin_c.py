@@ -41,6 +41,20 @@ def test_ssip_call_site(dropin_output):
             assert v == gold[k]
 
 
+def test_in_place_ssip_call_site(dropin_output):
+    """NTT_PLAN_IN_PLACE at the SSIP call site: the same outputs as SSIP (the reference's 2^26 values),
+    round trip through the in-place inverse."""
+    gold = dict(zip(GOLD["samp_idx_26"].tolist(), GOLD["samp_iota_26"].tolist()))
+    n = 1 << 26
+    assert len(dropin_output["INPLACE_SSIP"]) == 6
+    for log_n, k, v in dropin_output["INPLACE_SSIP"]:
+        k, v = int(k), int(v)
+        assert v == R.kat_xj(n, R.P469762049, 3, k)
+        if k in gold:
+            assert v == gold[k]
+    assert dropin_output["INPLACE_ROUNDTRIP"] == [["26", "ok"]]
+
+
 def test_gzkp256_call_site(dropin_output):
     got = {}
     for log_n, k, v in dropin_output["GZKP256"]:
