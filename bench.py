@@ -130,23 +130,18 @@ def cpu_baseline(field_id: int, limbs: int, log_n: int):
 
 
 def _cpu_reference_field(log_n: int = 22):
-    """The reference's own CPU path on its own field, P = 469762049, x_j = j (its input), 1 core:
-    GZKP-NTT.cu:30-48 itself (oracle/_ref, compiled from the reference sources; kind "reference")
-    when built, else its restatement oracle_ntt_u64 (kind "port")."""
+    """The reference's CPU path on its own field, P = 469762049, x_j = j (its input), 1 core, as the
+    restatement oracle_ntt_u64 of GZKP-NTT.cu:30-48 (kind "port").  The reference's own compiled code
+    (oracle/_ref) is a test-only checker and is never loaded into the bench process; the tests pin
+    the port against it (tests/test_oracle_ref.py, tests/golden/ref_p469762049.npz)."""
     import numpy as np
     from oracle import oracle_c as OC
-    from oracle import ref_c
     x = np.arange(1 << log_n, dtype=np.int64)
-    if ref_c.available():
-        kind, fn = "reference", (lambda v: ref_c.ntt(v))
-    else:
-        kind, fn = "port", (lambda v: OC.ntt_u64(v, 469762049, 3))
     t0 = time.perf_counter()
-    fn(x)
+    OC.ntt_u64(x, 469762049, 3)
     dt = time.perf_counter() - t0
-    return {"value": (1 << log_n) / dt, "unit": "field-elements/s", "cores": 1, "seconds": dt, "kind": kind,
-            "sample": f"one 2^{log_n}-point forward NTT over P469762049 (GZKP-NTT.cu NTT, "
-                      f"{'the reference code itself' if kind == 'reference' else 'restated'})"}
+    return {"value": (1 << log_n) / dt, "unit": "field-elements/s", "cores": 1, "seconds": dt, "kind": "port",
+            "sample": f"one 2^{log_n}-point forward NTT over P469762049 (GZKP-NTT.cu:30-48 restated)"}
 
 
 def load_traffic(tag: str):

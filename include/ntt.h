@@ -95,7 +95,17 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
  * palindrome the pass kernels accept (2^11 and 2^13 on the 1024-element tiles; P: 2^15, 2^17, 2^19
  * on its 8192-element tiles) and the rival schedules return NTT_ERR_ARG. */
 #define NTT_PLAN_IN_PLACE 16u
+/* Single-launch schedule (BASELINE config 2, "single-kernel self-sort-in-place"; the reference runs
+ * 2^20 as 4 launches, GZKP-NTT.cu:1509-1545): a 3-pass forward / inverse of a 4-limb BN254 / BLS12-381
+ * plan (2^18 .. 2^24) runs as ONE persistent launch; the passes' tiles are handed between workgroups
+ * through dependency counters instead of kernel boundaries (k_fused3).  Same contract and results as
+ * the default schedule; batch 1; other plans and calls ignore the flag.  ntt_plan_device_status
+ * reports a dependency wait that gave up (a watchdog; never expected). */
+#define NTT_PLAN_SINGLE_LAUNCH 32u
 int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags);
+/* Watchdog of NTT_PLAN_SINGLE_LAUNCH: *bad = non-zero if a launch since the last call had a tile
+ * give up waiting for its inputs (its output is then wrong).  Blocking; clears the word. */
+int ntt_plan_device_status(ntt_plan* plan, unsigned* bad);
 
 /* Modulus-generic plan, like big-num.cu's `prime` / `omega` kernel arguments (big-num.cu:68,173,260):
  * modulus and generator given as limbs64 little-endian 64-bit limbs. */

@@ -46,6 +46,16 @@
 
 namespace ntt {
 
+// 16-B write-through vector store (sc1: the line leaves this XCD's L2 at once, so a workgroup on any
+// XCD that acquires after the publishing counter reads it fresh; MI355X_MICROARCH.md § visibility,
+// the R1 publish form).  The compiler does not count inline-asm stores: the publisher drains them
+// with an explicit s_waitcnt vmcnt(0) before it signals.  s_nop 1: the store-data VGPR hazard.
+__device__ __forceinline__ void store_wt16(uint4* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const v4u v = {a, b, c, d};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+
 // ------------------------------------------------------------------------------ 29-bit engine
 // Twiddles are multiplied with Shoup's precomputed-quotient product (mulc29): a table entry holds
 // the canonical w and ws = floor(w * B / p), B = 2^(29L).  143 MADs per product for L = 9 instead
@@ -178,11 +188,12 @@ struct Eng29 {
     }
   }
   // x < BOUND p -> x < 2p (fits the HBM words: p < 2^255) -> HBM.  Between passes only.
-  template <int BOUND, bool FAST = false, int MW = W32>
+  // WT: write-through stores (the fused single-launch schedule hands the tile to other workgroups)
+  template <int BOUND, bool FAST = false, int MW = W32, bool WT = false>
   __device__ static __forceinline__ void store_lazy(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
                                                     const Args& A) {
     reduce<BOUND, 2, FAST>(x, A);
-    put<MW>(base, idx, x);
+    put<MW, WT>(base, idx, x);
   }
   // x < BOUND p -> canonical -> HBM
   template <int BOUND, bool FAST = false, int MW = W32>
@@ -191,13 +202,18 @@ struct Eng29 {
     reduce<BOUND, 1, FAST>(x, A);
     put<MW>(base, idx, x);
   }
-  template <int MW = W32>
+  template <int MW = W32, bool WT = false>
   __device__ static __forceinline__ void put(uint32_t* __restrict__ base, size_t idx, const uint32_t (&x)[W]) {
     uint32_t w[MW];
     unpack29<L, MW>(w, x);
     uint4* p = reinterpret_cast<uint4*>(base + idx * MW);
 #pragma unroll
-    for (int q = 0; q < MW / 4; ++q) p[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    for (int q = 0; q < MW / 4; ++q) {
+      if constexpr (WT)
+        store_wt16(p + q, w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+      else
+        p[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    }
   }
   __device__ static __forceinline__ void tload(Tw& t, const uint32_t* __restrict__ tab, size_t idx) {
     const uint4* p = reinterpret_cast<const uint4*>(tab + idx * TW);
@@ -344,9 +360,10 @@ struct Eng32 {
   static constexpr bool FASTRED = false;
   template <int FROM, int TO, bool FAST = false, bool R32 = true>
   __device__ static __forceinline__ void reduce(uint32_t (&)[W], const Args&) {}
-  template <int BOUND, bool FAST = false, int MW = MEMW_>
+  template <int BOUND, bool FAST = false, int MW = MEMW_, bool WT = false>
   __device__ static __forceinline__ void store_lazy(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
                                                     const Args& A) {
+    static_assert(!WT, "write-through scratch stores: Eng29 engines only (fused schedule)");
     store<BOUND, FAST, MW>(base, idx, x, A);
   }
   template <int BOUND, bool FAST = false, int MW = MEMW_>

@@ -90,6 +90,32 @@ struct PassArgs {
 };
 enum : uint32_t { FS_MAP_IN = 1u, FS_MAP_OUT = 2u, FS_IL = 4u };
 
+// Fused single-launch schedule of a 3-pass transform (k_fused3, BASELINE config 2's "single-kernel"):
+// one persistent launch runs pass 1's, pass 2's and the final pass's tiles, handed between
+// workgroups through counters instead of kernel boundaries.  Word layout of `sync` (zero before the
+// first launch; the last workgroup to leave re-zeroes it): [0] tile ticket, [1] workgroups exited,
+// [2] watchdog (non-zero: a dependency wait gave up), [3] spare, [4, 4 + n12) pass 1 -> 2 counters,
+// [4 + n12, 4 + n12 + n23) pass 2 -> final counters.
+struct FusedArgs {
+  uint32_t* sync;
+  uint32_t tiles;      // tiles per pass (n / TILE)
+  uint32_t nwg;        // workgroups launched
+  uint32_t k1_mask, k1_shift;  // pass-1 tile w: counter (w & k1_mask) >> k1_shift
+  uint32_t cg_log;             // pass-2 tile w: column group w mod 2^cg_log, block k1 = w >> cg_log
+  uint32_t k2_shift;           //   waits on counter (w mod 2^cg_log) >> k2_shift
+  uint32_t t3_log;             //   signals counter n12 + (k1 >> t3_log)
+  uint32_t r2;                 // final tile w: waits on counter n12 + (w >> r2)
+  uint32_t n12, n23;
+  uint32_t need12, need23;     // arrivals per counter
+};
+template <class E>
+hipError_t launch_fused3(int r1, int r2, int r3, const uint32_t* src, uint32_t* scratch, uint32_t* dst,
+                         const PassArgs<E>& A1, const PassArgs<E>& A2, const PassArgs<E>& A3, const FusedArgs& F,
+                         hipStream_t st);
+// workgroups one launch of k_fused3<E, r1, r2, r3> keeps resident on `device` (occupancy query x CUs)
+template <class E>
+hipError_t fused3_capacity(int r1, int r2, int r3, int device, uint32_t* wgs);
+
 template <class E, int KIND>
 hipError_t launch_pass_kind(int logr, const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t grid,
                             uint32_t batch, hipStream_t st);
@@ -137,6 +163,7 @@ struct DrevArgs {
   uint32_t mid_bits[4];  // middle digit widths of `mid`, least significant first (PassArgs::mid_bits)
   uint32_t mid_off[4];   // their bit offsets in midrev (PassArgs::mid_off)
   size_t batch_stride;   // 32-bit words between batched transforms
+  uint64_t unit0;        // first tile pair of this launch (launch_digitrev_swap chunks the grid)
 };
 template <class E>
 hipError_t launch_digitrev_swap(uint32_t* data, const DrevArgs& A, uint32_t batch, hipStream_t st);

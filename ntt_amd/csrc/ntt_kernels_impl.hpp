@@ -184,7 +184,7 @@ __device__ __forceinline__ uint32_t lds_slot(uint32_t c, uint32_t pi) {
 
 // Wave-uniform trivial twiddles.  Sub-stage s multiplies its outputs k = 1..Q-1 by w^(cp k) with
 // cp = g mod sigma_s.  When sigma_s divides the wave count, every cp class is whole waves: wave w
-// takes cp = (w + rot) mod sigma_s (rot = blockIdx.x, so that each SIMD -- which holds the same wave
+// takes cp = (w + rot) mod sigma_s (rot = the tile index, so that each SIMD -- which holds the same wave
 // slot of several workgroups -- gets its share of the cp = 0 waves), and the cp = 0 waves skip their
 // products (w^0 = 1) with a scalar branch.  NTT_UNIFORM_CP=0 keeps the lane-order mapping.
 #ifndef NTT_UNIFORM_CP
@@ -219,7 +219,7 @@ __device__ __forceinline__ void sub_map(uint32_t t, int j, uint32_t rot, uint32_
 template <class E, int LOGR, int T, int TE, int NT, int s, bool FAST, bool R32, bool LTW>
 __device__ __forceinline__ void substage(uint32_t (&x)[E::EPT][E::W], uint32_t (&cl)[E::EPT / 2],
                                          uint32_t (&pil)[E::EPT / 2], uint32_t* lds, const PassArgs<E>& A, int t,
-                                         const uint32_t* lds_tw) {
+                                         const uint32_t* lds_tw, uint32_t rot) {
   using S = Sched<LOGR, ept_log<E>()>;
   constexpr int EPT = E::EPT;
   constexpr int pqb = S::qb(s - 1), PQ = 1 << pqb, PG = EPT / PQ, psb = S::logsig(s - 1), plN = S::logN(s - 1);
@@ -242,7 +242,7 @@ __device__ __forceinline__ void substage(uint32_t (&x)[E::EPT][E::W], uint32_t (
     static_for<G>([&](auto J) {
       constexpr int j = J;
       uint32_t c, g;
-      sub_map<LOGR, ept_log<E>(), T, NT, EPT, s>(t, j, blockIdx.x, c, g);
+      sub_map<LOGR, ept_log<E>(), T, NT, EPT, s>(t, j, rot, c, g);
       const uint32_t rho = g >> sb, cp = g & ((1u << sb) - 1);
       static_for<Q>([&](auto D) {
         constexpr int d = D;
@@ -254,7 +254,7 @@ __device__ __forceinline__ void substage(uint32_t (&x)[E::EPT][E::W], uint32_t (
   static_for<G>([&](auto J) {
     constexpr int j = J;
     uint32_t c, g;
-    sub_map<LOGR, ept_log<E>(), T, NT, EPT, s>(t, j, blockIdx.x, c, g);
+    sub_map<LOGR, ept_log<E>(), T, NT, EPT, s>(t, j, rot, c, g);
     cl[j] = c;
     pil[j] = g;
   });
@@ -305,25 +305,44 @@ enum : int { PRO_NONE = 0, PRO_PW = 1, PRO_COSET = 2 };
 #ifndef NTT_COL_R32_BELOW
 #define NTT_COL_R32_BELOW 8
 #endif
+// LDS of one pass tile (words), and whether the pass stages its w_R^e table in LDS: E::LDS_TW
+// (parallel-load stage), not in a first pass with two-level outer twiddles (the P path's pass 1),
+// where it measured slower (profiles/r02_ldstw/)
+template <class E, int LOGR, int KIND>
+__host__ __device__ constexpr int pass_tile_te() {
+  return (KIND == KIND_SINGLE) ? (1 << LOGR) : (1 << tile_log_of<E>());
+}
+template <class E, int LOGR, int KIND>
+__host__ __device__ constexpr int pass_lds_words() {
+  return pass_tile_te<E, LOGR, KIND>() * LdsParts<E::LDSW, E::LDS_SPLIT>::max_words();
+}
+template <class E, int KIND, bool FULLTW>
+__host__ __device__ constexpr bool pass_ltw() {
+  return E::LDS_TW && !(KIND == KIND_COLUMN && !FULLTW);
+}
+
+// One workgroup tile of one pass: tile w (the workgroup index of a k_pass launch) of transform bq
+// (its blockIdx.y).  lds: pass_lds_words() words, lds_tw: 2^LOGR words when pass_ltw().  k_pass runs
+// one tile per workgroup; the fused single-launch schedule (k_fused3) runs several passes' tiles
+// in one persistent workgroup.
+// LOOPED (persistent workgroups, k_fused3): the thread index is re-read per tile through an opaque
+// copy, so that the compiler does not hoist every lane-dependent address out of the tile loop (held in
+// VGPRs across the whole loop, they spilled 200-380 B per thread; per tile they cost a few VALU ops).
 template <class E, int LOGR, int KIND, bool FULLTW, bool FAST, int PRO = PRO_NONE, bool SRC_USER = true,
-          int FSM = 0, bool SHTW = false>
-__global__ __launch_bounds__((1 << E::TILE_LOG) / E::EPT) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
-void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
-                                              const PassArgs<E> A) {
+          int FSM = 0, bool SHTW = false, bool WT = false, bool LOOPED = false>
+__device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                          const PassArgs<E>& A, const uint32_t w, const uint32_t bq,
+                                          uint32_t* __restrict__ lds, uint32_t* __restrict__ lds_tw) {
   constexpr int QB = ept_log<E>(), EPT = E::EPT;
   using S = Sched<LOGR, QB>;
   constexpr bool COLLIKE = KIND == KIND_COLUMN || KIND == KIND_STOCKHAM || KIND == KIND_DIT;  // column groups
-  constexpr int TE = (KIND == KIND_SINGLE) ? (1 << LOGR) : (1 << tile_log_of<E>());
+  constexpr int TE = pass_tile_te<E, LOGR, KIND>();
   constexpr int T = TE >> LOGR;  // columns (column pass) or blocks (final / single) per workgroup
   // reduce_top form (engines.hpp): radix-256 column passes are at the VGPR cap and keep the 64-bit one
   constexpr bool R32 = KIND != KIND_COLUMN || LOGR < NTT_COL_R32_BELOW;
   constexpr int NT = TE / EPT;   // threads
   static_assert(LOGR >= QB && T >= 1, "radix");
-  __shared__ __attribute__((aligned(16))) uint32_t lds[TE * LdsParts<E::LDSW, E::LDS_SPLIT>::max_words()];
-  // E::LDS_TW (parallel-load stage): this pass's w_R^e table in LDS -- not in a first pass with
-  // two-level outer twiddles (the P path's pass 1), where it measured slower (profiles/r02_ldstw/)
-  constexpr bool LTW = E::LDS_TW && !(KIND == KIND_COLUMN && !FULLTW);
-  __shared__ uint32_t lds_tw[LTW ? (1 << LOGR) : 1];
+  constexpr bool LTW = pass_ltw<E, KIND, FULLTW>();
 
   // HBM words per element: the caller's buffers hold E::MEMW, the plan's scratch and outer-twiddle
   // tables E::SCRW (8 for 256-bit values in the 48-B layout).  Column passes read the caller's
@@ -332,7 +351,8 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
   constexpr int SW = (KIND == KIND_COLUMN) ? (SRC_USER ? E::MEMW : E::SCRW) : (KIND == KIND_FINAL ? E::SCRW : E::MEMW);
   constexpr int DW = (KIND == KIND_COLUMN) ? E::SCRW : E::MEMW;
 
-  const int t = threadIdx.x;
+  int t = threadIdx.x;
+  if constexpr (LOOPED) asm volatile("" : "+v"(t));
   if (t >= NT) return;
   // Four-step addressing (PassArgs::fs, ntt_rplan_*): the first pass may read and the last pass may
   // write through the per-peer chunk maps, and Mode I runs 2^il interleaved transforms.  All flags
@@ -343,7 +363,6 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
   const bool map_in = FSM > 0 && IN_USER && (A.fs & FS_MAP_IN);
   const bool map_out = FSM > 0 && KIND != KIND_COLUMN && (A.fs & FS_MAP_OUT);
   const bool single_il = KIND == KIND_SINGLE && fs_il;  // one interleaved transform per workgroup
-  const uint32_t bq = blockIdx.y;
   const size_t bidx = (size_t)bq * (A.batch_stride / E::MEMW);  // first element of this transform
   if (!map_in && !single_il) src += bidx * SW;
   if (!map_out && !single_il) dst += bidx * DW;
@@ -372,7 +391,6 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
   uint32_t col0 = 0;   // column pass: column index (within block) of local column 0
   uint32_t mid = 0, k10 = 0, midrev = 0;  // final pass
   uint32_t b0 = 0, tb_log = 0;            // final pass, Mode I: first transform, log2 transforms per WG
-  const uint32_t w = blockIdx.x;
   if constexpr (COLLIKE) {
     const uint32_t log_s = A.log_blk - LOGR;
     const uint32_t groups_log = log_s - __builtin_ctz(T);  // column groups per block (log)
@@ -493,11 +511,11 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
   }
 
   // ------------------------------------------------------------------ sub-stages 1..nsub-1 via LDS
-  if constexpr (S::nsub > 1) substage<E, LOGR, T, TE, NT, 1, FAST, R32, LTW>(x, cl, pil, lds, A, t, lds_tw);
-  if constexpr (S::nsub > 2) substage<E, LOGR, T, TE, NT, 2, FAST, R32, LTW>(x, cl, pil, lds, A, t, lds_tw);
-  if constexpr (S::nsub > 3) substage<E, LOGR, T, TE, NT, 3, FAST, R32, LTW>(x, cl, pil, lds, A, t, lds_tw);
-  if constexpr (S::nsub > 4) substage<E, LOGR, T, TE, NT, 4, FAST, R32, LTW>(x, cl, pil, lds, A, t, lds_tw);
-  if constexpr (S::nsub > 5) substage<E, LOGR, T, TE, NT, 5, FAST, R32, LTW>(x, cl, pil, lds, A, t, lds_tw);
+  if constexpr (S::nsub > 1) substage<E, LOGR, T, TE, NT, 1, FAST, R32, LTW>(x, cl, pil, lds, A, t, lds_tw, w);
+  if constexpr (S::nsub > 2) substage<E, LOGR, T, TE, NT, 2, FAST, R32, LTW>(x, cl, pil, lds, A, t, lds_tw, w);
+  if constexpr (S::nsub > 3) substage<E, LOGR, T, TE, NT, 3, FAST, R32, LTW>(x, cl, pil, lds, A, t, lds_tw, w);
+  if constexpr (S::nsub > 4) substage<E, LOGR, T, TE, NT, 4, FAST, R32, LTW>(x, cl, pil, lds, A, t, lds_tw, w);
+  if constexpr (S::nsub > 5) substage<E, LOGR, T, TE, NT, 5, FAST, R32, LTW>(x, cl, pil, lds, A, t, lds_tw, w);
   static_assert(S::nsub <= 6, "sub-stages");
 
   // ------------------------------------------------------------------ output
@@ -555,7 +573,7 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
             E::mulv(v, tl.w, A.F);
           }
           pos = colbase + c + ((size_t)kn << log_s);
-          E::template store_lazy<E::MUL_OUT, FAST, DW>(dst, NTT_NOMEM(pos), v, A.F);  // scratch: < 2p, read by the next pass
+          E::template store_lazy<E::MUL_OUT, FAST, DW, WT>(dst, NTT_NOMEM(pos), v, A.F);  // scratch: < 2p, read by the next pass
         } else if constexpr (KIND == KIND_FINAL) {
           if (fs_il) {
             const uint32_t k1 = k10 + (c >> tb_log), b = b0 + (c & ((1u << tb_log) - 1));
@@ -592,6 +610,195 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
     });
   }
 }
+
+template <class E, int LOGR, int KIND, bool FULLTW, bool FAST, int PRO = PRO_NONE, bool SRC_USER = true,
+          int FSM = 0, bool SHTW = false>
+__global__ __launch_bounds__((1 << E::TILE_LOG) / E::EPT) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
+void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, const PassArgs<E> A) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[pass_lds_words<E, LOGR, KIND>()];
+  __shared__ uint32_t lds_tw[pass_ltw<E, KIND, FULLTW>() ? (1 << LOGR) : 1];
+  pass_tile<E, LOGR, KIND, FULLTW, FAST, PRO, SRC_USER, FSM, SHTW>(src, dst, A, blockIdx.x, blockIdx.y, lds, lds_tw);
+}
+
+// ---------------------------------------------------------------------------- fused 3-pass launch
+// BASELINE config 2 asks for the 2^20 transform as a single kernel (the reference's SSIP schedule is
+// 4 launches at 2^20, GZKP-NTT.cu:1509-1545).  k_fused3 runs the three passes of a 3-pass schedule in
+// ONE persistent launch.  Workgroups take tiles from one ticket counter in pass-major order (pass 1's
+// tiles, then pass 2's, then the final pass's); a tile waits only for the tiles it reads, through
+// counters keyed by the dependency structure of the four-step passes:
+//   * pass-2 tile (block k1, column group g) reads columns g T2 + [0, T2) + s2 j2 of every j2 < R2,
+//     written by the pass-1 tiles whose columns mod s2 (= 2^r3) fall in the same U-column unit
+//     (U = max(T1, T2)): s2 / U counters, each reached by (U / T1) R2 pass-1 tiles;
+//   * a final tile (T3 adjacent k1, one k2) reads every column of those k1 blocks: counters keyed by
+//     k1 >> log T3 (R1 / T3 of them), each reached by T3 (s2 / T2) pass-2 tiles.
+// Deadlock-free at any residency: a tile waits only for tiles with smaller tickets, which are held
+// by running workgroups whose own waits are on smaller tickets still (pass 1 waits on nothing).
+// Hand-off (MI355X_MICROARCH.md § visibility, publish form R1): scratch stores are write-through
+// (sc1), every wave drains them (s_waitcnt vmcnt(0)), a workgroup barrier, then one lane's agent-scope
+// counter add; the consumer polls relaxed, takes ONE agent-scope acquire, waits, barrier, plain loads.
+// Every dependency wait is bounded (watchdog word, then the tile runs anyway: wrong output, no hang),
+// so every wave reaches the exit; the last workgroup out re-zeroes the counters for the next launch.
+__device__ __forceinline__ void fused_publish(uint32_t* cnt) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through stores are done
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void fused_wait(uint32_t* cnt, uint32_t need, uint32_t* watchdog) {
+  if (threadIdx.x == 0) {
+    uint32_t spins = 0;
+    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins == (1u << 24)) {  // ~1 s: give up (reported through the watchdog word)
+        __hip_atomic_store(watchdog, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+template <class E>
+struct FusedKArgs {
+  const uint32_t* src;
+  uint32_t* scratch;
+  uint32_t* dst;
+  PassArgs<E> A1, A2, A3;
+  FusedArgs F;
+};
+static_assert(sizeof(FusedKArgs<Eng256>) <= 4096, "kernel argument segment");
+// The kernel arguments re-addressed per tile through an opaque copy of the kernarg pointer, so that
+// the persistent loops do not keep every pass's uniform arguments live across the loop (with the
+// LOOPED thread index above: 0-16 B of spills instead of 200-380 B).
+template <class E>
+__device__ __forceinline__ const FusedKArgs<E>& fused_kargs() {
+  typedef const __attribute__((address_space(4))) FusedKArgs<E>* KP;
+  KP p = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return *(const FusedKArgs<E>*)p;
+}
+
+template <class E, int R1, int R2, int R3>
+__global__ __launch_bounds__((1 << E::TILE_LOG) / E::EPT) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
+void k_fused3(const FusedKArgs<E> K) {
+  static_assert(E::FASTRED && E::SHOUP_OUTER && !E::LDS_TW, "fused schedule: FAST 256-bit engines");
+  constexpr int LW = pass_lds_words<E, R1, KIND_COLUMN>();
+  static_assert(LW == pass_lds_words<E, R3, KIND_FINAL>(), "one tile size");
+  __shared__ __attribute__((aligned(16))) uint32_t lds[LW];
+  __shared__ uint32_t lds_tw[1];
+  __shared__ uint32_t s_ticket;
+  const FusedArgs& F = K.F;
+  uint32_t* const cnt12 = F.sync + 4;
+  uint32_t* const cnt23 = F.sync + 4 + F.n12;
+  const uint32_t t = threadIdx.x, total = 3 * F.tiles;
+  if (t == 0) s_ticket = __hip_atomic_fetch_add(F.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  uint32_t tk = s_ticket;
+  // the next ticket: its add is issued before the tile, its value used after it
+  auto ticket = [&]() -> uint32_t {
+    return t == 0 ? __hip_atomic_fetch_add(F.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+  };
+  auto advance = [&](uint32_t next) {
+    __syncthreads();  // every wave is done with this tile's LDS and s_ticket
+    if (t == 0) s_ticket = next;
+    __syncthreads();
+    tk = s_ticket;
+  };
+  // tickets are handed out in pass-major order, so a workgroup's tickets only grow: one loop per pass
+  while (tk < F.tiles) {  // pass 1: the caller's buffer -> scratch
+    const uint32_t next = ticket(), w = tk;
+    const FusedKArgs<E>& L = fused_kargs<E>();
+    pass_tile<E, R1, KIND_COLUMN, true, true, PRO_NONE, true, 0, false, true, true>(L.src, L.scratch, L.A1, w, 0,
+                                                                                      lds, lds_tw);
+    fused_publish(cnt12 + ((w & F.k1_mask) >> F.k1_shift));
+    advance(next);
+  }
+  while (tk < 2 * F.tiles) {  // pass 2: scratch in place (Shoup-pair outer twiddles)
+    const uint32_t next = ticket(), w = tk - F.tiles, g = w & ((1u << F.cg_log) - 1);
+    fused_wait(cnt12 + (g >> F.k2_shift), F.need12, F.sync + 2);
+    const FusedKArgs<E>& L = fused_kargs<E>();
+    pass_tile<E, R2, KIND_COLUMN, true, true, PRO_NONE, true, 0, true, true, true>(L.scratch, L.scratch, L.A2, w, 0,
+                                                                                     lds, lds_tw);
+    fused_publish(cnt23 + ((w >> F.cg_log) >> F.t3_log));
+    advance(next);
+  }
+  while (tk < total) {  // final pass: scratch -> the caller's buffer, natural order
+    const uint32_t next = ticket(), w = tk - 2 * F.tiles;
+    fused_wait(cnt23 + (w >> F.r2), F.need23, F.sync + 2);
+    const FusedKArgs<E>& L = fused_kargs<E>();
+    pass_tile<E, R3, KIND_FINAL, false, true, PRO_NONE, true, 0, false, false, true>(L.scratch, L.dst, L.A3, w, 0,
+                                                                                       lds, lds_tw);
+    advance(next);
+  }
+  if (t == 0 && __hip_atomic_fetch_add(F.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == F.nwg - 1) {
+    // the last workgroup out: nobody touches the counters again in this launch
+    const uint32_t words = 4 + F.n12 + F.n23;
+    for (uint32_t i = 0; i < words; ++i)
+      if (i != 2) __hip_atomic_store(F.sync + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <class E>
+hipError_t launch_fused3(int r1, int r2, int r3, const uint32_t* src, uint32_t* scratch, uint32_t* dst,
+                         const PassArgs<E>& A1, const PassArgs<E>& A2, const PassArgs<E>& A3, const FusedArgs& F,
+                         hipStream_t st) {
+  if constexpr (!(E::FASTRED && E::SHOUP_OUTER && !E::LDS_TW && E::TILE_LOG == 10 && E::EPT == 4)) {
+    return hipErrorInvalidValue;
+  } else {
+    const dim3 g(F.nwg), b((1 << E::TILE_LOG) / E::EPT);
+#define NTT_FUSED_CASE(a, c, d)                                                                   \
+  if (r1 == a && r2 == c && r3 == d) {                                                            \
+    hipLaunchKernelGGL((k_fused3<E, a, c, d>), g, b, 0, st, FusedKArgs<E>{src, scratch, dst, A1, A2, A3, F});    \
+    return hipGetLastError();                                                                     \
+  }
+    NTT_FUSED_CASE(6, 6, 6)
+    NTT_FUSED_CASE(7, 6, 6)
+    NTT_FUSED_CASE(7, 7, 6)
+    NTT_FUSED_CASE(7, 7, 7)
+    NTT_FUSED_CASE(8, 7, 7)
+    NTT_FUSED_CASE(8, 8, 7)
+    NTT_FUSED_CASE(8, 8, 8)
+#undef NTT_FUSED_CASE
+    return hipErrorInvalidValue;
+  }
+}
+
+template <class E>
+hipError_t fused3_capacity(int r1, int r2, int r3, int device, uint32_t* wgs) {
+  if constexpr (!(E::FASTRED && E::SHOUP_OUTER && !E::LDS_TW && E::TILE_LOG == 10 && E::EPT == 4)) {
+    return hipErrorInvalidValue;
+  } else {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return hipErrorInvalidValue;
+    const int threads = (1 << E::TILE_LOG) / E::EPT;
+    hipError_t e = hipErrorInvalidValue;
+#define NTT_FUSED_OCC(a, c, d)                                                                         \
+  if (r1 == a && r2 == c && r3 == d)                                                                   \
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_fused3<E, a, c, d>), \
+                                                     threads, 0);
+    NTT_FUSED_OCC(6, 6, 6)
+    NTT_FUSED_OCC(7, 6, 6)
+    NTT_FUSED_OCC(7, 7, 6)
+    NTT_FUSED_OCC(7, 7, 7)
+    NTT_FUSED_OCC(8, 7, 7)
+    NTT_FUSED_OCC(8, 8, 7)
+    NTT_FUSED_OCC(8, 8, 8)
+#undef NTT_FUSED_OCC
+    if (e != hipSuccess) return e;
+    *wgs = (uint32_t)(cus * per);
+    return hipSuccess;
+  }
+}
+
+// Element-wise kernels run as grid-stride loops over at most 2^20 workgroups of 256 threads:
+// grid.x * blockDim.x stays far below HIP's 2^32-thread launch limit at every supported size
+// (2^32-element BLS12-381 vectors included).
+__host__ __device__ constexpr uint32_t grid_1d(size_t count) {
+  return (uint32_t)((count + 255) / 256 < (size_t(1) << 20) ? (count + 255) / 256 : (size_t(1) << 20));
+}
+#define NTT_GRID_STRIDE(idx, count) \
+  for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < (count); idx += (size_t)gridDim.x * blockDim.x)
 
 // O(n^2) transform for tiny n (n <= 4): X_k = sum_j x_j w^(jk); tw_int holds w^e, e < n.
 template <class E>
@@ -631,30 +838,30 @@ __global__ void k_build_tw(uint32_t* __restrict__ out, size_t count, uint32_t lo
                            const uint32_t* __restrict__ lo, const uint32_t* __restrict__ hi, uint32_t lo_bits,
                            const typename E::Args F, const uint32_t* __restrict__ clo,
                            const uint32_t* __restrict__ chi) {
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= count) return;
-  const size_t k = (idx >> log_t) & ((1ull << log_r) - 1);
-  const size_t c = ((idx >> (log_t + log_r)) << log_t) + (idx & ((1ull << log_t) - 1));
-  const size_t e = (c * k) << log_m;
-  typename E::Tw a, b;
-  E::tload(a, lo, (uint32_t)(e & ((1ull << lo_bits) - 1)));
-  E::tload(b, hi, (uint32_t)(e >> lo_bits));
-  E::mul(a.w, b, F);
-  if (clo) {  // c^col R_e = clo[col & mask] * chi[col >> lo_bits]; mulv removes one R_e
-    typename E::Tw u, v;
-    E::tload(u, clo, (uint32_t)(c & ((1ull << lo_bits) - 1)));
-    E::tload(v, chi, (uint32_t)(c >> lo_bits));
-    E::mul(u.w, v, F);
-    E::mulv(a.w, u.w, F);
+  NTT_GRID_STRIDE(idx, count) {
+    const size_t k = (idx >> log_t) & ((1ull << log_r) - 1);
+    const size_t c = ((idx >> (log_t + log_r)) << log_t) + (idx & ((1ull << log_t) - 1));
+    const size_t e = (c * k) << log_m;
+    typename E::Tw a, b;
+    E::tload(a, lo, (uint32_t)(e & ((1ull << lo_bits) - 1)));
+    E::tload(b, hi, (uint32_t)(e >> lo_bits));
+    E::mul(a.w, b, F);
+    if (clo) {  // c^col R_e = clo[col & mask] * chi[col >> lo_bits]; mulv removes one R_e
+      typename E::Tw u, v;
+      E::tload(u, clo, (uint32_t)(c & ((1ull << lo_bits) - 1)));
+      E::tload(v, chi, (uint32_t)(c >> lo_bits));
+      E::mul(u.w, v, F);
+      E::mulv(a.w, u.w, F);
+    }
+    E::template store<E::MUL_OUT, false, E::SCRW>(out, idx, a.w, F);  // outer-twiddle tables: E::SCRW words
   }
-  E::template store<E::MUL_OUT, false, E::SCRW>(out, idx, a.w, F);  // outer-twiddle tables: E::SCRW words
 }
 
 template <class E>
 hipError_t launch_build_tw(uint32_t* out, size_t count, uint32_t log_r, uint32_t log_t, uint32_t log_m,
                            const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits, const typename E::Args& F,
                            hipStream_t st, const uint32_t* clo, const uint32_t* chi) {
-  hipLaunchKernelGGL((k_build_tw<E>), dim3((uint32_t)((count + 255) / 256)), dim3(256), 0, st, out, count, log_r,
+  hipLaunchKernelGGL((k_build_tw<E>), dim3(grid_1d(count)), dim3(256), 0, st, out, count, log_r,
                      log_t, log_m, lo, hi, lo_bits, F, clo, chi);
   return hipGetLastError();
 }
@@ -667,35 +874,35 @@ __global__ void k_build_tw_sh(uint32_t* __restrict__ out, size_t count, uint32_t
                               uint32_t log_m, const uint32_t* __restrict__ lo, const uint32_t* __restrict__ hi,
                               uint32_t lo_bits, const typename E::Args F, const uint32_t* __restrict__ pinvB) {
   constexpr int L = E::W;
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= count) return;
-  const size_t k = (idx >> log_t) & ((1ull << log_r) - 1);
-  const size_t c = ((idx >> (log_t + log_r)) << log_t) + (idx & ((1ull << log_t) - 1));
-  const size_t e = (c * k) << log_m;
-  typename E::Tw a, b;
-  E::tload(a, lo, (uint32_t)(e & ((1ull << lo_bits) - 1)));
-  E::tload(b, hi, (uint32_t)(e >> lo_bits));
-  E::mul(a.w, b, F);  // w B mod p, < 3p
-  uint32_t wr[L], w[L], one[L], t[L], ws[L], pib[L];
+  NTT_GRID_STRIDE(idx, count) {
+    const size_t k = (idx >> log_t) & ((1ull << log_r) - 1);
+    const size_t c = ((idx >> (log_t + log_r)) << log_t) + (idx & ((1ull << log_t) - 1));
+    const size_t e = (c * k) << log_m;
+    typename E::Tw a, b;
+    E::tload(a, lo, (uint32_t)(e & ((1ull << lo_bits) - 1)));
+    E::tload(b, hi, (uint32_t)(e >> lo_bits));
+    E::mul(a.w, b, F);  // w B mod p, < 3p
+    uint32_t wr[L], w[L], one[L], t[L], ws[L], pib[L];
 #pragma unroll
-  for (int i = 0; i < L; ++i) {
-    wr[i] = a.w[i];
-    one[i] = i == 0 ? 1u : 0u;
-    pib[i] = pinvB[i];
+    for (int i = 0; i < L; ++i) {
+      wr[i] = a.w[i];
+      one[i] = i == 0 ? 1u : 0u;
+      pib[i] = pinvB[i];
+    }
+    E::template reduce<4, 1, false>(wr, F);  // canonical w B mod p
+#pragma unroll
+    for (int i = 0; i < L; ++i) w[i] = wr[i];
+    E::mulv(w, one, F);  // w, < 3p
+    E::template reduce<4, 1, false>(w, F);
+    neg29<L>(t, wr);
+    mullo29<L>(ws, t, pib);
+    uint32_t o[E::TW];
+#pragma unroll
+    for (int i = 0; i < E::TW; ++i) o[i] = i < L ? w[i] : (i < 2 * L ? ws[i - L] : 0u);
+    uint4* p = reinterpret_cast<uint4*>(out + idx * E::TW);
+#pragma unroll
+    for (int q = 0; q < E::TW / 4; ++q) p[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
   }
-  E::template reduce<4, 1, false>(wr, F);  // canonical w B mod p
-#pragma unroll
-  for (int i = 0; i < L; ++i) w[i] = wr[i];
-  E::mulv(w, one, F);  // w, < 3p
-  E::template reduce<4, 1, false>(w, F);
-  neg29<L>(t, wr);
-  mullo29<L>(ws, t, pib);
-  uint32_t o[E::TW];
-#pragma unroll
-  for (int i = 0; i < E::TW; ++i) o[i] = i < L ? w[i] : (i < 2 * L ? ws[i - L] : 0u);
-  uint4* p = reinterpret_cast<uint4*>(out + idx * E::TW);
-#pragma unroll
-  for (int q = 0; q < E::TW / 4; ++q) p[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
 }
 
 template <class E>
@@ -705,7 +912,7 @@ hipError_t launch_build_tw_sh(uint32_t* out, size_t count, uint32_t log_r, uint3
   if constexpr (!E::SHOUP_OUTER) {
     return hipErrorInvalidValue;
   } else {
-    hipLaunchKernelGGL((k_build_tw_sh<E>), dim3((uint32_t)((count + 255) / 256)), dim3(256), 0, st, out, count,
+    hipLaunchKernelGGL((k_build_tw_sh<E>), dim3(grid_1d(count)), dim3(256), 0, st, out, count,
                        log_r, log_t, log_m, lo, hi, lo_bits, F, pinvB);
     return hipGetLastError();
   }
@@ -723,22 +930,22 @@ struct DigitRev {
 template <int MEMW>
 __global__ void k_digitrev(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t log_n,
                            DigitRev D) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >> log_n) return;
-  size_t j = 0, rem = i;
-  uint32_t top = log_n;
-  for (uint32_t q = 0; q < D.nd; ++q) {
-    top -= D.r[q];
-    j |= (rem & ((1ull << D.r[q]) - 1)) << top;
-    rem >>= D.r[q];
-  }
-  if constexpr (MEMW % 4 == 0) {
+  NTT_GRID_STRIDE(i, (size_t(1) << log_n)) {
+    size_t j = 0, rem = i;
+    uint32_t top = log_n;
+    for (uint32_t q = 0; q < D.nd; ++q) {
+      top -= D.r[q];
+      j |= (rem & ((1ull << D.r[q]) - 1)) << top;
+      rem >>= D.r[q];
+    }
+    if constexpr (MEMW % 4 == 0) {
 #pragma unroll
-    for (int q = 0; q < MEMW / 4; ++q)
-      reinterpret_cast<uint4*>(dst + i * MEMW)[q] = reinterpret_cast<const uint4*>(src + j * MEMW)[q];
-  } else {
+      for (int q = 0; q < MEMW / 4; ++q)
+        reinterpret_cast<uint4*>(dst + i * MEMW)[q] = reinterpret_cast<const uint4*>(src + j * MEMW)[q];
+    } else {
 #pragma unroll
-    for (int q = 0; q < MEMW; ++q) dst[i * MEMW + q] = src[j * MEMW + q];
+      for (int q = 0; q < MEMW; ++q) dst[i * MEMW + q] = src[j * MEMW + q];
+    }
   }
 }
 
@@ -752,7 +959,7 @@ hipError_t launch_bitrev(const uint32_t* src, uint32_t* dst, uint32_t log_n, con
   for (uint32_t q = 0; q < nd; ++q) sum += (D.r[q] = digits[q]);
   if (sum != log_n) return hipErrorInvalidValue;
   const size_t n = 1ull << log_n;
-  hipLaunchKernelGGL((k_digitrev<E::MEMW>), dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, src, dst, log_n,
+  hipLaunchKernelGGL((k_digitrev<E::MEMW>), dim3(grid_1d(n)), dim3(256), 0, st, src, dst, log_n,
                      D);
   return hipGetLastError();
 }
@@ -764,15 +971,15 @@ template <class E>
 __global__ void k_build_fs_tw(uint32_t* __restrict__ out, uint32_t log_rows, uint32_t log_cols, uint64_t row0,
                               uint64_t col0, uint32_t log_n, const uint32_t* __restrict__ lo,
                               const uint32_t* __restrict__ hi, uint32_t lo_bits, const typename E::Args F) {
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >> (log_rows + log_cols)) return;
-  const uint64_t a = idx >> log_cols, b = idx & ((1ull << log_cols) - 1);
-  const uint64_t e = ((row0 + a) * (col0 + b)) & ((1ull << log_n) - 1);
-  typename E::Tw x, y;
-  E::tload(x, lo, (uint32_t)(e & ((1ull << lo_bits) - 1)));
-  E::tload(y, hi, (uint32_t)(e >> lo_bits));
-  E::mul(x.w, y, F);
-  E::template store<E::MUL_OUT, false, E::SCRW>(out, idx, x.w, F);
+  NTT_GRID_STRIDE(idx, (size_t(1) << (log_rows + log_cols))) {
+    const uint64_t a = idx >> log_cols, b = idx & ((1ull << log_cols) - 1);
+    const uint64_t e = ((row0 + a) * (col0 + b)) & ((1ull << log_n) - 1);
+    typename E::Tw x, y;
+    E::tload(x, lo, (uint32_t)(e & ((1ull << lo_bits) - 1)));
+    E::tload(y, hi, (uint32_t)(e >> lo_bits));
+    E::mul(x.w, y, F);
+    E::template store<E::MUL_OUT, false, E::SCRW>(out, idx, x.w, F);
+  }
 }
 
 template <class E>
@@ -780,7 +987,7 @@ hipError_t launch_build_fs_tw(uint32_t* out, uint32_t log_rows, uint32_t log_col
                               uint32_t log_n, const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits,
                               const typename E::Args& F, hipStream_t st) {
   const size_t count = 1ull << (log_rows + log_cols);
-  hipLaunchKernelGGL((k_build_fs_tw<E>), dim3((uint32_t)((count + 255) / 256)), dim3(256), 0, st, out, log_rows,
+  hipLaunchKernelGGL((k_build_fs_tw<E>), dim3(grid_1d(count)), dim3(256), 0, st, out, log_rows,
                      log_cols, row0, col0, log_n, lo, hi, lo_bits, F);
   return hipGetLastError();
 }
@@ -797,19 +1004,19 @@ __global__ void k_twiddle_pack(const uint32_t* __restrict__ src, uint32_t* __res
                                uint32_t log_len, uint32_t log_bw, uint64_t row0, uint32_t log_n,
                                const uint32_t* __restrict__ lo, const uint32_t* __restrict__ hi, uint32_t lo_bits,
                                const typename E::Args F, uint64_t peer_stride) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (1ull << (log_rows + log_len))) return;
-  const uint64_t a = i >> log_len, b = i & ((1ull << log_len) - 1);
-  const uint64_t e = ((row0 + a) * b) & ((1ull << log_n) - 1);
-  uint32_t x[E::W];
-  typename E::Tw w, h;
-  E::load(x, src, i);
-  E::tload(w, lo, (uint32_t)(e & ((1ull << lo_bits) - 1)));
-  E::tload(h, hi, (uint32_t)(e >> lo_bits));
-  E::mul(w.w, h, F);
-  E::mulv(x, w.w, F);
-  const size_t blk = b >> log_bw, off = b & ((1ull << log_bw) - 1);
-  E::template store<E::MUL_OUT>(dst, blk * peer_stride + (a << log_bw) + off, x, F);
+  NTT_GRID_STRIDE(i, (1ull << (log_rows + log_len))) {
+    const uint64_t a = i >> log_len, b = i & ((1ull << log_len) - 1);
+    const uint64_t e = ((row0 + a) * b) & ((1ull << log_n) - 1);
+    uint32_t x[E::W];
+    typename E::Tw w, h;
+    E::load(x, src, i);
+    E::tload(w, lo, (uint32_t)(e & ((1ull << lo_bits) - 1)));
+    E::tload(h, hi, (uint32_t)(e >> lo_bits));
+    E::mul(w.w, h, F);
+    E::mulv(x, w.w, F);
+    const size_t blk = b >> log_bw, off = b & ((1ull << log_bw) - 1);
+    E::template store<E::MUL_OUT>(dst, blk * peer_stride + (a << log_bw) + off, x, F);
+  }
 }
 
 // Coset scale (low-degree-extension step): data[j] *= c^j over `batch` vectors of 2^log_n elements,
@@ -819,24 +1026,24 @@ template <class E>
 __global__ void k_scale_pow(uint32_t* __restrict__ data, uint32_t log_n, const uint32_t* __restrict__ lo_s,
                             const uint32_t* __restrict__ hi, uint32_t lo_bits, const typename E::Args F,
                             size_t batch_stride) {
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >> log_n) return;
-  uint32_t* d = data + (size_t)blockIdx.y * batch_stride;
-  uint32_t x[E::W];
-  typename E::Tw w, h;
-  E::load(x, d, j);
-  E::tload(w, lo_s, (uint32_t)(j & ((1ull << lo_bits) - 1)));
-  E::tload(h, hi, (uint32_t)(j >> lo_bits));
-  E::mul(w.w, h, F);
-  E::mulv(x, w.w, F);
-  E::template store<E::MUL_OUT>(d, j, x, F);
+  NTT_GRID_STRIDE(j, (size_t(1) << log_n)) {
+    uint32_t* d = data + (size_t)blockIdx.y * batch_stride;
+    uint32_t x[E::W];
+    typename E::Tw w, h;
+    E::load(x, d, j);
+    E::tload(w, lo_s, (uint32_t)(j & ((1ull << lo_bits) - 1)));
+    E::tload(h, hi, (uint32_t)(j >> lo_bits));
+    E::mul(w.w, h, F);
+    E::mulv(x, w.w, F);
+    E::template store<E::MUL_OUT>(d, j, x, F);
+  }
 }
 
 template <class E>
 hipError_t launch_scale_pow(uint32_t* data, uint32_t log_n, uint32_t batch, const uint32_t* lo_s, const uint32_t* hi,
                             uint32_t lo_bits, const typename E::Args& F, hipStream_t st) {
   const size_t n = 1ull << log_n;
-  const dim3 grid((uint32_t)((n + 255) / 256), batch);
+  const dim3 grid(grid_1d(n), batch);
   hipLaunchKernelGGL((k_scale_pow<E>), grid, dim3(256), 0, st, data, log_n, lo_s, hi, lo_bits, F,
                      n * (size_t)E::MEMW);
   return hipGetLastError();
@@ -898,7 +1105,7 @@ hipError_t launch_twiddle_pack(const uint32_t* src, uint32_t* dst, uint32_t log_
                                uint32_t log_bw, uint64_t row0, uint32_t log_n, const uint32_t* lo, const uint32_t* hi,
                                uint32_t lo_bits, const typename E::Args& F, uint64_t peer_stride, hipStream_t st) {
   const size_t total = 1ull << (log_rows + log_len);
-  hipLaunchKernelGGL((k_twiddle_pack<E>), dim3((uint32_t)((total + 255) / 256)), dim3(256), 0, st, src, dst, log_rows,
+  hipLaunchKernelGGL((k_twiddle_pack<E>), dim3(grid_1d(total)), dim3(256), 0, st, src, dst, log_rows,
                      log_len, log_bw, row0, log_n, lo, hi, lo_bits, F, peer_stride);
   return hipGetLastError();
 }
@@ -926,7 +1133,7 @@ __global__ __launch_bounds__(256) void k_digitrev_swap(uint32_t* data, DrevArgs 
   constexpr int SL = MW + 1;  // LDS slot stride (words): odd, so transposed reads spread over banks
   __shared__ uint32_t tile[2][256 * SL];
   const uint32_t tl = A.tb_log, ntl = A.R - tl;
-  const uint64_t u = blockIdx.x;
+  const uint64_t u = A.unit0 + blockIdx.x;
   const uint32_t nm = (1u << ntl) - 1;
   const uint32_t lo = (uint32_t)(u & nm), hi = (uint32_t)((u >> ntl) & nm);
   // diagonal order (A.diag): I = lo, J = lo + hi, so that neighbouring workgroups differ in both tile
@@ -992,10 +1199,17 @@ __global__ __launch_bounds__(256) void k_digitrev_swap(uint32_t* data, DrevArgs 
 template <class E>
 hipError_t launch_digitrev_swap(uint32_t* data, const DrevArgs& A, uint32_t batch, hipStream_t st) {
   if (A.R < A.tb_log || 2 * A.R > A.log_n || A.tb_log > 4) return hipErrorInvalidValue;
-  const uint64_t units = 1ull << (A.log_n - 2 * A.tb_log);
-  if (units > 0xffffffffull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((k_digitrev_swap<E::MEMW>), dim3((uint32_t)units, batch), dim3(256), 0, st, data, A);
-  return hipGetLastError();
+  // grid.x * blockDim.x must stay below 2^32 threads: 2^(log_n - 2 tb_log) tile pairs go as launches
+  // of at most 2^23 workgroups (A.unit0 = the first pair of the launch)
+  const uint64_t units = 1ull << (A.log_n - 2 * A.tb_log), chunk = 1ull << 23;
+  for (uint64_t u0 = 0; u0 < units; u0 += chunk) {
+    DrevArgs B = A;
+    B.unit0 = u0;
+    const uint64_t cnt = units - u0 < chunk ? units - u0 : chunk;
+    hipLaunchKernelGGL((k_digitrev_swap<E::MEMW>), dim3((uint32_t)cnt, batch), dim3(256), 0, st, data, B);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 // ---------------------------------------------------------------------------- utility kernels
@@ -1021,58 +1235,58 @@ __device__ __forceinline__ uint64_t fill_index(size_t i, const FillMap& m) {
 template <int MEMW>
 __global__ void k_fill_random(uint32_t* __restrict__ dst, size_t n, uint64_t seed, uint32_t nrand, uint32_t top_bits,
                               FillMap fm) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t j = fill_index(i, fm);
-  if constexpr (MEMW == 2) {
-    const uint64_t v = splitmix64((seed << 32) + 4 * j) & ((1ull << top_bits) - 1);
-    reinterpret_cast<uint2*>(dst)[i] = make_uint2((uint32_t)v, 0u);
-  } else {
-    uint32_t v[MEMW];
+  NTT_GRID_STRIDE(i, n) {
+    const uint64_t j = fill_index(i, fm);
+    if constexpr (MEMW == 2) {
+      const uint64_t v = splitmix64((seed << 32) + 4 * j) & ((1ull << top_bits) - 1);
+      reinterpret_cast<uint2*>(dst)[i] = make_uint2((uint32_t)v, 0u);
+    } else {
+      uint32_t v[MEMW];
 #pragma unroll
-    for (int i = 0; i < MEMW / 2; ++i) {
-      uint64_t limb = 0;
-      if ((uint32_t)i < nrand) {
-        limb = splitmix64((seed << 32) + 4 * j + i);
-        if ((uint32_t)i + 1 == nrand && top_bits < 64) limb &= (1ull << top_bits) - 1;
+      for (int l = 0; l < MEMW / 2; ++l) {
+        uint64_t limb = 0;
+        if ((uint32_t)l < nrand) {
+          limb = splitmix64((seed << 32) + 4 * j + l);
+          if ((uint32_t)l + 1 == nrand && top_bits < 64) limb &= (1ull << top_bits) - 1;
+        }
+        v[2 * l] = (uint32_t)limb;
+        v[2 * l + 1] = (uint32_t)(limb >> 32);
       }
-      v[2 * i] = (uint32_t)limb;
-      v[2 * i + 1] = (uint32_t)(limb >> 32);
-    }
-    uint4* p = reinterpret_cast<uint4*>(dst + i * MEMW);
+      uint4* p = reinterpret_cast<uint4*>(dst + i * MEMW);
 #pragma unroll
-    for (int q = 0; q < MEMW / 4; ++q) p[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+      for (int q = 0; q < MEMW / 4; ++q) p[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    }
   }
 }
 
 template <int MEMW>
 __global__ void k_fill_iota(uint32_t* __restrict__ dst, size_t n, FillMap fm) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t j = fill_index(i, fm);
-  if constexpr (MEMW == 2) {
-    reinterpret_cast<uint2*>(dst)[i] = make_uint2((uint32_t)j, (uint32_t)((uint64_t)j >> 32));
-  } else {
-    uint4* p = reinterpret_cast<uint4*>(dst + i * MEMW);
-    p[0] = make_uint4((uint32_t)j, (uint32_t)((uint64_t)j >> 32), 0u, 0u);
+  NTT_GRID_STRIDE(i, n) {
+    const uint64_t j = fill_index(i, fm);
+    if constexpr (MEMW == 2) {
+      reinterpret_cast<uint2*>(dst)[i] = make_uint2((uint32_t)j, (uint32_t)((uint64_t)j >> 32));
+    } else {
+      uint4* p = reinterpret_cast<uint4*>(dst + i * MEMW);
+      p[0] = make_uint4((uint32_t)j, (uint32_t)((uint64_t)j >> 32), 0u, 0u);
 #pragma unroll
-    for (int q = 1; q < MEMW / 4; ++q) p[q] = make_uint4(0u, 0u, 0u, 0u);
+      for (int q = 1; q < MEMW / 4; ++q) p[q] = make_uint4(0u, 0u, 0u, 0u);
+    }
   }
 }
 
 template <class E>
 __global__ void k_pointwise_mul(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint32_t* __restrict__ c,
                                 size_t n, const typename E::Args F, const uint32_t* __restrict__ r2) {
-  const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  uint32_t x[E::W], y[E::W];
-  typename E::Tw z;  // R_e mod p as a twiddle: mulv leaves x y / R_e
-  E::load(x, a, j);
-  E::load(y, b, j);
-  E::tload(z, r2, 0);
-  E::mulv(x, y, F);
-  E::mul(x, z, F);
-  E::template store<E::MUL_OUT>(c, j, x, F);
+  NTT_GRID_STRIDE(j, n) {
+    uint32_t x[E::W], y[E::W];
+    typename E::Tw z;  // R_e mod p as a twiddle: mulv leaves x y / R_e
+    E::load(x, a, j);
+    E::load(y, b, j);
+    E::tload(z, r2, 0);
+    E::mulv(x, y, F);
+    E::mul(x, z, F);
+    E::template store<E::MUL_OUT>(c, j, x, F);
+  }
 }
 
 // Canonical-range check (the reference's padded-store `BAD LIMB` trap, impl_cuda.cu:1402-1408, as a
@@ -1081,21 +1295,21 @@ __global__ void k_pointwise_mul(const uint32_t* __restrict__ a, const uint32_t* 
 template <int MEMW>
 __global__ void k_count_noncanonical(const uint32_t* __restrict__ d, size_t n, ModWords<MEMW> p,
                                      unsigned long long* __restrict__ bad) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t* e = d + i * MEMW;
-  int cmp = 0;  // sign of e - p, decided by the most significant differing word
+  NTT_GRID_STRIDE(i, n) {
+    const uint32_t* e = d + i * MEMW;
+    int cmp = 0;  // sign of e - p, decided by the most significant differing word
 #pragma unroll
-  for (int k = MEMW - 1; k >= 0; --k)
-    if (cmp == 0 && e[k] != p.w[k]) cmp = e[k] < p.w[k] ? -1 : 1;
-  if (cmp >= 0) atomicAdd(bad, 1ull);
+    for (int k = MEMW - 1; k >= 0; --k)
+      if (cmp == 0 && e[k] != p.w[k]) cmp = e[k] < p.w[k] ? -1 : 1;
+    if (cmp >= 0) atomicAdd(bad, 1ull);
+  }
 }
 
 template <class E>
 hipError_t launch_count_noncanonical(const uint32_t* d, size_t n, const ModWords<E::MEMW>& p,
                                      unsigned long long* bad, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL((k_count_noncanonical<E::MEMW>), dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, d, n, p,
+  hipLaunchKernelGGL((k_count_noncanonical<E::MEMW>), dim3(grid_1d(n)), dim3(256), 0, st, d, n, p,
                      bad);
   return hipGetLastError();
 }
@@ -1230,7 +1444,7 @@ hipError_t launch_naive(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A
 template <class E>
 hipError_t launch_fill(int kind, uint32_t* dst, size_t n, uint64_t seed, uint32_t nrand, uint32_t top_bits,
                        uint64_t row0, uint32_t log_inner, uint32_t log_stride, hipStream_t st) {
-  const uint32_t blocks = (uint32_t)((n + 255) / 256);
+  const uint32_t blocks = grid_1d(n);
   const FillMap fm{row0, log_inner, log_stride};
   if (kind == 0)
     hipLaunchKernelGGL((k_fill_iota<E::MEMW>), dim3(blocks), dim3(256), 0, st, dst, n, fm);
@@ -1242,7 +1456,7 @@ hipError_t launch_fill(int kind, uint32_t* dst, size_t n, uint64_t seed, uint32_
 template <class E>
 hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, size_t n, const typename E::Args& F,
                             const uint32_t* d_r2, hipStream_t st) {
-  const uint32_t blocks = (uint32_t)((n + 255) / 256);
+  const uint32_t blocks = grid_1d(n);
   hipLaunchKernelGGL((k_pointwise_mul<E>), dim3(blocks), dim3(256), 0, st, a, b, c, n, F, d_r2);
   return hipGetLastError();
 }
@@ -1255,6 +1469,11 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
 #define NTT_EXTERN_KIND(E, KIND)                                                                                     \
   extern template hipError_t launch_pass_kind<E, KIND>(int, const uint32_t*, uint32_t*, const PassArgs<E>&, uint32_t, \
                                                        uint32_t, hipStream_t);
+
+#define NTT_INSTANTIATE_FUSED(E)                                                                                  \
+  template hipError_t launch_fused3<E>(int, int, int, const uint32_t*, uint32_t*, uint32_t*, const PassArgs<E>&,     \
+                                       const PassArgs<E>&, const PassArgs<E>&, const FusedArgs&, hipStream_t);      \
+  template hipError_t fused3_capacity<E>(int, int, int, int, uint32_t*);
 
 #define NTT_INSTANTIATE(E)                                                                                         \
   NTT_EXTERN_KIND(E, KIND_COLUMN)                                                                                  \

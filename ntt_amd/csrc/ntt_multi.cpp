@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
@@ -38,15 +39,24 @@ struct Rccl {
   ncclResult_t (*GroupEnd)() = nullptr;
   ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
-  bool ok() const { return CommInitAll && CommDestroy && AllToAll && GroupStart && GroupEnd && Send && Recv; }
+  ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
+  bool ok() const {
+    return CommInitAll && CommDestroy && AllToAll && GroupStart && GroupEnd && Send && Recv && CommAbort;
+  }
 };
 
 const Rccl& rccl() {
   static const Rccl r = [] {
     Rccl x;
     void* h = RTLD_DEFAULT;
-    // NTT_RCCL_LIBRARY: an explicit RCCL (or a fault-injecting stand-in, tests/test_gpu_mplan_faults.py)
+    // NTT_RCCL_LIBRARY: an explicit RCCL (or a fault-injecting stand-in, tests/test_gpu_mplan_faults.py).
+    // Absolute paths only (no search-path lookup), and the override is announced on stderr.
     if (const char* lib = getenv("NTT_RCCL_LIBRARY"); lib && *lib) {
+      if (lib[0] != '/') {
+        fprintf(stderr, "libntt: NTT_RCCL_LIBRARY must be an absolute path; ignored: %s\n", lib);
+        return x;
+      }
+      fprintf(stderr, "libntt: multi-GPU collectives from NTT_RCCL_LIBRARY=%s\n", lib);
       h = dlopen(lib, RTLD_NOW | RTLD_LOCAL);
       if (!h) return x;
     } else if (!dlsym(h, "ncclCommInitAll")) {
@@ -61,6 +71,7 @@ const Rccl& rccl() {
     x.GroupEnd = reinterpret_cast<decltype(x.GroupEnd)>(dlsym(h, "ncclGroupEnd"));
     x.Send = reinterpret_cast<decltype(x.Send)>(dlsym(h, "ncclSend"));
     x.Recv = reinterpret_cast<decltype(x.Recv)>(dlsym(h, "ncclRecv"));
+    x.CommAbort = reinterpret_cast<decltype(x.CommAbort)>(dlsym(h, "ncclCommAbort"));
     return x;
   }();
   return r;
@@ -81,6 +92,9 @@ struct ntt_mplan {
   std::vector<hipEvent_t> ev_ready;   // per device: compute -> communication ordering
   std::vector<hipEvent_t> ev_done;    // per device and piece: arrival of piece i (kMaxPieces each)
   unsigned pieces = 1;
+  // set when an exchange failed: the communicators were aborted (a peer may have posted its part of
+  // the collective) and every later call returns NTT_ERR_RCCL
+  bool broken = false;
 
   ~ntt_mplan() {
     int cur = 0;
@@ -119,6 +133,23 @@ struct DeviceGuard {
 // above kMaxPeerBytes are exchanged as grouped ncclSend/ncclRecv pieces instead.
 constexpr size_t kMaxPeerBytes = size_t(1) << 30;
 
+// A call failed inside a grouped exchange.  If it failed on device g > 0, devices 0..g-1 already
+// posted their part: the closed group launched a partial all-to-all whose kernels wait for peers that
+// never come, and a stream drain would block forever.  Aborting every communicator ends those
+// operations (RCCL's documented recovery); the plan is then unusable and every later call returns
+// NTT_ERR_RCCL.  The caller's drain() follows.
+int abort_comms(ntt_mplan* m) {
+  const Rccl& R = rccl();
+  for (size_t g = 0; g < m->comm.size(); ++g) {
+    if (!m->comm[g]) continue;
+    (void)hipSetDevice(m->dev[g]);
+    (void)R.CommAbort(m->comm[g]);
+    m->comm[g] = nullptr;
+  }
+  m->broken = true;
+  return NTT_ERR_RCCL;
+}
+
 // All-to-all of per-peer chunks of `words` 64-bit words: send[g] = [G][words] -> recv[g] = [G][words].
 int exchange(ntt_mplan* m, const std::vector<void*>& send, const std::vector<void*>& recv, size_t words,
              void* const* streams) {
@@ -148,7 +179,7 @@ int exchange(ntt_mplan* m, const std::vector<void*>& send, const std::vector<voi
   // always close the group: the calls already issued for other devices are launched (or dropped) by
   // RCCL as a unit, never left pending in the thread's group state
   const ncclResult_t end = R.GroupEnd();
-  return (st == ncclSuccess && end == ncclSuccess) ? NTT_OK : NTT_ERR_RCCL;
+  return (st == ncclSuccess && end == ncclSuccess) ? NTT_OK : abort_comms(m);
 }
 
 size_t chunk_words(const ntt_mplan* m) {  // per-peer chunk of one vector: r * c elements
@@ -179,7 +210,7 @@ int exchange_rows(ntt_mplan* m, const std::vector<void*>& send, const std::vecto
       }
   }
   const ncclResult_t end = R.GroupEnd();
-  return (st == ncclSuccess && end == ncclSuccess) ? NTT_OK : NTT_ERR_RCCL;
+  return (st == ncclSuccess && end == ncclSuccess) ? NTT_OK : abort_comms(m);
 }
 
 // comm stream of every device waits for the work enqueued so far on its compute stream
@@ -387,6 +418,7 @@ int ntt_mplan_create(ntt_mplan** out, int field_id, unsigned log_n, unsigned lim
 
 int ntt_forward_multi(ntt_mplan* m, void* const* d_data, void* const* streams) {
   if (!m || !d_data) return NTT_ERR_ARG;
+  if (m->broken) return NTT_ERR_RCCL;
   DeviceGuard guard;
   void* const* v[1] = {d_data};
   const int rc = forward_vectors(m, v, 1, streams);
@@ -395,6 +427,7 @@ int ntt_forward_multi(ntt_mplan* m, void* const* d_data, void* const* streams) {
 
 int ntt_inverse_multi(ntt_mplan* m, void* const* d_data, void* const* streams) {
   if (!m || !d_data) return NTT_ERR_ARG;
+  if (m->broken) return NTT_ERR_RCCL;
   DeviceGuard guard;
   const int rc = inverse_vector(m, d_data, nullptr, d_data, streams);
   return rc ? drain(m, streams, rc) : NTT_OK;
@@ -402,6 +435,7 @@ int ntt_inverse_multi(ntt_mplan* m, void* const* d_data, void* const* streams) {
 
 int ntt_polymul_multi(ntt_mplan* m, void* const* d_a, void* const* d_b, void* const* d_c, void* const* streams) {
   if (!m || !d_a || !d_b || !d_c) return NTT_ERR_ARG;
+  if (m->broken) return NTT_ERR_RCCL;
   DeviceGuard guard;
   if (int rc = ensure_pair_buffers(m)) return rc;
   bool same = true;  // squaring: a == b on every device -> one forward transform

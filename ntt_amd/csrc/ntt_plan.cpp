@@ -102,6 +102,7 @@ struct PlanBase {
   virtual unsigned passes_for(unsigned log_x) const = 0;
   virtual int coset(void* d, const uint64_t* shift, unsigned limbs64, bool inverse, hipStream_t st) = 0;
   virtual int count_noncanonical(const void* d, uint64_t count, uint64_t* bad, hipStream_t st) = 0;
+  virtual int device_status(unsigned* bad) = 0;
   uint64_t n = 0;
   unsigned flags = 0;
   unsigned log_n = 0, elem_bytes = 0, npass = 0;
@@ -372,6 +373,7 @@ struct PlanImpl final : PlanBase {
     if (d_bad) hipFree(d_bad);
     if (d_coset) hipFree(d_coset);
     if (d_coset_full) hipFree(d_coset_full);
+    if (d_sync) hipFree(d_sync);
     for (auto& row : ev)
       for (auto& e : row)
         if (e) hipEventDestroy(e);
@@ -953,9 +955,12 @@ struct PlanImpl final : PlanBase {
         work = d_scratch;
       }
       const uint32_t grid = (uint32_t)((n << il) >> tile_log_of<E>());
+      // the passes' arguments: column passes 0..npass-2, then the final pass
+      PassArgs<E> PA[8];
       unsigned blk = log_n;
-      for (unsigned i = 0; i + 1 < npass && e == hipSuccess; ++i) {
-        PassArgs<E> A = base_args(inverse);
+      for (unsigned i = 0; i + 1 < npass; ++i) {
+        PassArgs<E>& A = PA[i];
+        A = base_args(inverse);
         A.tw_int = d_tab + off_int[i];
         A.tw_lo = d_tab + (inverse ? off_los_i : off_los_f);
         A.tw_hi = d_tab + (inverse ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
@@ -978,27 +983,38 @@ struct PlanImpl final : PlanBase {
         A.log_m = log_n - blk;
         A.src_user = (i == 0) ? 1u : 0u;
         set_fs(A, i == 0 ? FS_MAP_IN : 0u);
-        const uint32_t* src = (i == 0) ? in : work;
-        e = launch_pass<E>(KIND_COLUMN, (int)r[i], src, work, A, grid, batch, st);
-        mark(st);
         blk -= r[i];
       }
-      if (e == hipSuccess) {
-        PassArgs<E> A = base_args(inverse);
-        A.tw_int = d_tab + off_int[npass - 1];
-        A.r1 = r[0];
-        A.nmid = npass - 2;
-        // middle digits k_2..k_{p-1}, least significant (k_{p-1}) first
-        for (unsigned m = 0; m < A.nmid; ++m) {
-          const unsigned idx = npass - 2 - m;  // pass index (0-based) of digit k_{idx+1}
-          A.mid_bits[m] = r[idx];
-          unsigned off = 0;
-          for (unsigned j = 1; j < idx; ++j) off += r[j];
-          A.mid_off[m] = off;
+      PassArgs<E>& A = PA[npass - 1];
+      A = base_args(inverse);
+      A.tw_int = d_tab + off_int[npass - 1];
+      A.r1 = r[0];
+      A.nmid = npass - 2;
+      // middle digits k_2..k_{p-1}, least significant (k_{p-1}) first
+      for (unsigned m = 0; m < A.nmid; ++m) {
+        const unsigned idx = npass - 2 - m;  // pass index (0-based) of digit k_{idx+1}
+        A.mid_bits[m] = r[idx];
+        unsigned off = 0;
+        for (unsigned j = 1; j < idx; ++j) off += r[j];
+        A.mid_off[m] = off;
+      }
+      set_fs(A, FS_MAP_OUT);
+      if (io) A.tw_epi = static_cast<const uint32_t*>(io->tw_epi);
+      if (inplace) A.flags |= 2u;
+      if constexpr (std::is_same_v<E, Eng256>) {  // the engine k_fused3 is instantiated for
+        if (!io && !inplace && batch == 1 && fused_enabled() && fused_ready(PA)) {
+          // one persistent launch for the three passes (NTT_PLAN_SINGLE_LAUNCH, k_fused3)
+          e = launch_fused3<E>((int)r[0], (int)r[1], (int)r[2], in, work, out, PA[0], PA[1], PA[2], fused_args(), st);
+          mark(st);
+          return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
         }
-        set_fs(A, FS_MAP_OUT);
-        if (io) A.tw_epi = static_cast<const uint32_t*>(io->tw_epi);
-        if (inplace) A.flags |= 2u;
+      }
+      for (unsigned i = 0; i + 1 < npass && e == hipSuccess; ++i) {
+        const uint32_t* src = (i == 0) ? in : work;
+        e = launch_pass<E>(KIND_COLUMN, (int)r[i], src, work, PA[i], grid, batch, st);
+        mark(st);
+      }
+      if (e == hipSuccess) {
         e = launch_pass<E>(KIND_FINAL, (int)r[npass - 1], work, out, A, grid, batch, st);
         mark(st);
         if (inplace && e == hipSuccess) {
@@ -1020,6 +1036,74 @@ struct PlanImpl final : PlanBase {
       }
     }
     return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+  }
+
+  // ---- fused single-launch schedule (NTT_PLAN_SINGLE_LAUNCH, k_fused3 in ntt_kernels_impl.hpp)
+  uint32_t* d_sync = nullptr;  // FusedArgs::sync words (zeroed at creation; each launch leaves them zeroed)
+  FusedArgs fargs{};
+  bool fused_built = false, fused_ok = false;
+  // NTT_SINGLE_LAUNCH=1 / =0 in the environment forces the schedule on / off for every plan (A/B)
+  bool fused_enabled() const {
+    static const int env = [] {
+      const char* v = getenv("NTT_SINGLE_LAUNCH");
+      return v && *v ? atoi(v) : -1;
+    }();
+    return env >= 0 ? env > 0 : (flags & NTT_PLAN_SINGLE_LAUNCH) != 0;
+  }
+  // 3-pass FAST 256-bit plans whose passes 1 and 2 take full tables (pass 2: Shoup pairs), and whose
+  // radices the fused kernel is instantiated for; built on first use
+  bool fused_ready(const PassArgs<E>* PA) {
+    if (!fused_built) {
+      fused_built = true;
+      fused_ok = build_fused();
+    }
+    return fused_ok && PA[0].tw_full && PA[1].tw_full && PA[1].tw_sh && !PA[0].src2 && !PA[0].tw_in;
+  }
+  bool build_fused() {
+    if constexpr (!std::is_same_v<E, Eng256>) {
+      return false;
+    } else {
+    if (npass != 3 || !use_full || !d_full_sh || !full_sh_ok[1] || !Ff.red_ok) return false;
+    const unsigned tl = tile_log_of<E>();
+    uint32_t cap = 0;
+    if (fused3_capacity<E>((int)r[0], (int)r[1], (int)r[2], device, &cap) != hipSuccess || cap == 0) return false;
+    const unsigned r1 = r[0], r2 = r[1], r3 = r[2];
+    const unsigned lt1 = tl - r1, lt2 = tl - r2, lt3 = tl - r3, lu = lt1 > lt2 ? lt1 : lt2;
+    if (r3 < lu || r1 < lt3) return false;  // schedule_ok guarantees both; kept as the kernel's contract
+    FusedArgs F{};
+    F.tiles = (uint32_t)(n >> tl);
+    F.nwg = F.tiles < cap ? F.tiles : cap;
+    F.k1_mask = (1u << (r3 - lt1)) - 1;
+    F.k1_shift = lu - lt1;
+    F.cg_log = r3 - lt2;
+    F.k2_shift = lu - lt2;
+    F.t3_log = lt3;
+    F.r2 = r2;
+    F.n12 = 1u << (r3 - lu);
+    F.n23 = 1u << (r1 - lt3);
+    F.need12 = 1u << (lu - lt1 + r2);
+    F.need23 = 1u << r2;
+    const size_t words = (4 + F.n12 + F.n23 + 3) & ~size_t(3);
+    if (hipMalloc(&d_sync, words * 4) != hipSuccess) {
+      d_sync = nullptr;
+      return false;
+    }
+    if (hipMemset(d_sync, 0, words * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return false;
+    F.sync = d_sync;
+    fargs = F;
+    return true;
+    }
+  }
+  const FusedArgs& fused_args() const { return fargs; }
+  // watchdog of the fused schedule: non-zero when a dependency wait gave up (then cleared)
+  int device_status(unsigned* bad) override {
+    *bad = 0;
+    if (!d_sync) return NTT_OK;
+    uint32_t w = 0;
+    if (hipMemcpy(&w, d_sync + 2, 4, hipMemcpyDeviceToHost) != hipSuccess) return NTT_ERR_HIP;
+    if (w && hipMemset(d_sync + 2, 0, 4) != hipSuccess) return NTT_ERR_HIP;
+    *bad = w;
+    return NTT_OK;
   }
 
   // ---- distributed four-step pieces (ntt_rplan, ntt_amd/csrc/ntt_rplan.cpp)
@@ -1293,6 +1377,11 @@ int ntt_pointwise_mul(ntt_plan* plan, const void* a, const void* b, void* c, voi
 
 int ntt_count_noncanonical(ntt_plan* plan, const void* d, uint64_t count, uint64_t* bad, void* s) {
   return on_device(plan, [&](PlanBase& P) { return P.count_noncanonical(d, count, bad, S(s)); });
+}
+
+int ntt_plan_device_status(ntt_plan* plan, unsigned* bad) {
+  if (!bad) return set_err(NTT_ERR_ARG);
+  return on_device(plan, [&](PlanBase& P) { return P.device_status(bad); });
 }
 
 int ntt_polymul(ntt_plan* plan, void* a, void* b, void* c, void* s) {

@@ -22,6 +22,7 @@ NTT_PLAN_MONTGOMERY_IO = 2
 NTT_PLAN_STOCKHAM = 4
 NTT_PLAN_GZKP = 8
 NTT_PLAN_IN_PLACE = 16
+NTT_PLAN_SINGLE_LAUNCH = 32
 
 # Every symbol declared in include/ntt.h with its ctypes prototype: (restype, argtypes).
 _vp = C.c_void_p
@@ -63,6 +64,7 @@ PROTOTYPES = {
     "ntt_mplan_set_pieces": (C.c_int, [_vp, C.c_uint]),
     "ntt_mplan_destroy": (C.c_int, [_vp]),
     "ntt_count_noncanonical": (C.c_int, [_vp, _vp, C.c_uint64, C.POINTER(C.c_uint64), _vp]),
+    "ntt_plan_device_status": (C.c_int, [_vp, C.POINTER(C.c_uint)]),
     "ntt_inverse_pointwise_batch": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint, _vp]),
     "ntt_twiddle_pack_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint, C.c_uint, C.c_uint, C.c_uint64, C.c_int, C.c_uint64,
                                       _vp]),

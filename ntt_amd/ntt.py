@@ -80,7 +80,7 @@ class NTTPlan:
     def __init__(self, field_id: int = 1, log_n: int = 10, limbs64: int = 4, device: int = 0,
                  modulus: Optional[int] = None, generator: Optional[int] = None, twiddle_only: bool = False,
                  montgomery_io: bool = False, stockham: bool = False, gzkp: bool = False,
-                 in_place: bool = False):
+                 in_place: bool = False, single_launch: bool = False):
         self._lib = _L.load()
         self.log_n = int(log_n)
         self.n = 1 << self.log_n
@@ -100,6 +100,8 @@ class NTTPlan:
         # in_place: no plan scratch, palindromic passes + tile-swap digit reversal (the reference's
         # self-sort-in-place property, GZKP-NTT.cu:1359-1449; ntt.h NTT_PLAN_IN_PLACE)
         flags |= _L.NTT_PLAN_IN_PLACE if in_place else 0
+        # single_launch: 3-pass transforms as one persistent launch (BASELINE config 2's single kernel)
+        flags |= _L.NTT_PLAN_SINGLE_LAUNCH if single_launch else 0
         self.montgomery_io = bool(montgomery_io)
         if modulus is None:
             st = self._lib.ntt_plan_create_ex(C.byref(h), int(field_id), self.log_n, self.limbs64, self.device, flags)
@@ -144,6 +146,12 @@ class NTTPlan:
         _L.check(self._lib.ntt_inverse(self._h, C.c_void_p(t.data_ptr()), _stream_ptr(stream, t.device)),
                  "ntt_inverse")
         return t
+
+    def device_status(self) -> int:
+        """Watchdog word of the single-launch schedule (non-zero: a tile gave up waiting); clears it."""
+        v = C.c_uint()
+        _L.check(self._lib.ntt_plan_device_status(self._h, C.byref(v)), "ntt_plan_device_status")
+        return v.value
 
     def count_noncanonical(self, t: torch.Tensor, stream=None) -> int:
         """Number of elements of t that are not < p (the transforms' input contract); blocking."""

@@ -23,9 +23,13 @@ _libs: dict = {}
 
 
 def build() -> bool:
-    """Build oracle/_ref from the reference sources when they are present; True if the libs exist."""
+    """Build oracle/_ref from the reference sources when they are present; True if the libs exist.
+    Never fatal: a failed reference compile leaves the checker absent (the committed fixtures in
+    tests/golden/ still pin the oracle), it does not fail the product build."""
     if os.path.isdir(os.path.join(REF_SRC, "src")):
-        subprocess.run(["make", "-C", HERE, "-s", "ref", f"REF={REF_SRC}"], check=True)
+        r = subprocess.run(["make", "-C", HERE, "-s", "ref", f"REF={REF_SRC}"], capture_output=True, text=True)
+        if r.returncode != 0:
+            print(f"oracle/_ref not built (test-only checker): {r.stderr.strip()[-400:]}")
     return available()
 
 

@@ -2,7 +2,8 @@
 
 * 2^24 random vectors compared with the threaded C oracle (oracle_ntt_mp_par, a restatement of
   GZKP-NTT.cu:30-48 pinned in test_oracle.py / test_oracle_ref.py): BN254 forward and inverse (the
-  headline), BLS12-381 Fr forward and inverse in the 6 x 64-bit layout (C3), the 8-B P path at 2^26;
+  headline), BLS12-381 Fr forward and inverse in the 4 and 6 x 64-bit layouts (C3), the 8-B P path
+  at 2^26;
 * C4's four-step at 2^28 over 8 virtual ranks (one GPU, exchange = device copies): the closed-form
   KAT of x_j = j at sampled k of the gathered column layout, plus the inverse round trip;
 * the single-process multi-GPU plan (ntt_mplan_*, RCCL) at 2^26 and 2^28 on the visible devices;
@@ -34,7 +35,7 @@ def _host(t, L):
     return t.cpu().numpy().view(np.uint64).reshape(-1, L)
 
 
-@pytest.mark.parametrize("fid,L,seed", [(1, 4, 24), (2, 6, 3)])
+@pytest.mark.parametrize("fid,L,seed", [(1, 4, 24), (2, 6, 3), (2, 4, 3)])
 def test_2pow24_elementwise_vs_threaded_oracle(fid, L, seed):
     p, g = R.FIELDS[fid]
     pl = _plan(fid, 24, L)

@@ -44,13 +44,66 @@ print("HEALTHY")
 '''
 
 
+def _build_stub(stub, src):
+    if not os.path.exists(stub) or os.path.getmtime(stub) < os.path.getmtime(src):
+        subprocess.run(["gcc", "-shared", "-fPIC", "-O2", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-o",
+                        stub, src, "-L/opt/rocm/lib", "-lamdhip64"], check=True)
+
+
 def test_rccl_failure_is_reported_and_drained():
     stub = os.path.join(ROOT, "tests", "c", "librccl_stub.so")
     src = os.path.join(ROOT, "tests", "c", "rccl_stub.c")
-    if not os.path.exists(stub) or os.path.getmtime(stub) < os.path.getmtime(src):
-        subprocess.run(["gcc", "-shared", "-fPIC", "-O2", "-o", stub, src], check=True)
+    _build_stub(stub, src)
     env = dict(os.environ, NTT_RCCL_LIBRARY=stub)
     r = subprocess.run([sys.executable, "-c", f"ROOT = {ROOT!r}\n" + CHILD], env=env, capture_output=True,
                        text=True, timeout=180)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     assert r.stdout.count("RCCL-ERROR") == 3 and "HEALTHY" in r.stdout
+
+
+# A failure on device g > 0 of a grouped exchange: device 0's part is posted and
+# "waits for its peers" (the stand-in blocks its stream until ncclCommAbort), device 1's call fails.
+# The plan must abort every communicator before draining, return NTT_ERR_RCCL instead of hanging, and
+# refuse later calls.  Two "devices" are the one GPU twice (the stand-in accepts any device list).
+CHILD_MID = r"""
+import ctypes, sys, time
+sys.path.insert(0, ROOT)
+import torch
+from ntt_amd.distributed import MultiPlan
+from ntt_amd.lib import NTTError
+mp = MultiPlan(1, 14, 4, devices=[0, 0], pieces=PIECES)
+xs = mp.fill(mp.empty(), "random", seed=1)
+torch.cuda.synchronize()
+t0 = time.time()
+try:
+    mp.forward(xs)
+    print("NO-ERROR"); sys.exit(3)
+except NTTError as e:
+    assert e.status == -3, e.status
+dt = time.time() - t0
+stub = ctypes.CDLL(STUB)
+print("ABORTS", stub.stub_aborts(), "HUNG", stub.stub_hung(), "SECONDS", round(dt, 2), flush=True)
+for call in (lambda: mp.forward(xs), lambda: mp.inverse(xs)):
+    try:
+        call(); print("NO-ERROR-AFTER"); sys.exit(4)
+    except NTTError as e:
+        assert e.status == -3, e.status
+del mp
+torch.cuda.synchronize()
+print("DONE")
+"""
+
+
+@pytest.mark.parametrize("pieces", [1, 2])
+def test_rccl_failure_on_second_device_aborts_instead_of_hanging(pieces):
+    stub = os.path.join(ROOT, "tests", "c", "librccl_stub.so")
+    src = os.path.join(ROOT, "tests", "c", "rccl_stub.c")
+    _build_stub(stub, src)
+    env = dict(os.environ, NTT_RCCL_LIBRARY=stub, NTT_STUB_OK_CALLS="1")
+    code = f"ROOT = {ROOT!r}\nSTUB = {stub!r}\nPIECES = {pieces}\n" + CHILD_MID
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    line = [l for l in r.stdout.splitlines() if l.startswith("ABORTS")][0].split()
+    aborts, hung, secs = int(line[1]), int(line[3]), float(line[5])
+    assert aborts == 2 and hung == 0 and secs < 15, line
+    assert "DONE" in r.stdout
