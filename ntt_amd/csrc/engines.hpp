@@ -302,107 +302,127 @@ struct Eng29 {
 };
 
 // ------------------------------------------------------------------------------ 32-bit engine
-// N x 32-bit limbs, canonical residues, CIOS/FIPS Montgomery (field.hpp).  Used for the 1-limb
-// P469762049 `long long` path (MEMW = 2).  Twiddles are stored in Montgomery form (w R), so
-// mont_mul(x, w R) = x w; every value stays canonical and the lazy-bound parameters are ignored.
+// One 32-bit limb: the P469762049 `long long` path (MEMW = 2), the reference's own field
+// (GZKP-NTT.cu:7-8) and any odd modulus p < 2^30.  Values live in [0, 2p) between operations
+// (Harvey's lazy butterflies: 4p < 2^32, so a + b and a - b + 2p never wrap) and are canonical in
+// the caller's HBM buffers; the plan scratch holds the lazy value.
+//   * twiddle x element: Shoup's product with a table entry (w, floor(w 2^32 / p)):
+//     q = mulhi(x, w'), r = x w - q p (mod 2^32) in [0, 2p) for any 32-bit x -- 4 VALU ops
+//     (v_mul_hi_u32, 2 x v_mul_lo_u32, v_sub_u32);
+//   * variable x variable (outer-twiddle tables in the element format, pointwise products):
+//     Montgomery with R = 2^32, r = hi(x y) - hi(m p) + p in (0, 2p) for x y < 2^32 p -- 6 ops;
+//   * reduction 2p -> p (and 4p -> 2p): min(x, x - p) as unsigned -- 2 ops, no compare.
+// The former CIOS / 64-bit-carry form took 127 VALU ops per element in a radix-256 column pass.
 template <int N, int MEMW_, int SCR_ = 0>
 struct Eng32 {
-  static constexpr int W = N;
+  static_assert(N == 1, "the 32-bit engine is the 1-limb path (p < 2^30)");
+  static constexpr int W = 1;
   static constexpr int MEMW = MEMW_;
   // 1-limb P path: values < 2^31, so the plan's scratch and tables hold 4 B per element where the
   // caller's `long long` layout holds 8 (HBM-bound path: a third less traffic per transform).
   // SCR_ != 0 forces the scratch width (EngPI: the caller's 8 B, for NTT_PLAN_IN_PLACE)
-  static constexpr int SCRW = SCR_ ? SCR_ : ((N == 1 && NTT_P_SCRATCH32) ? 1 : MEMW_);
-  static constexpr int TW = N;
-  static constexpr int LDSW = N;
-  static constexpr int IN = 4;
+  static constexpr int SCRW = SCR_ ? SCR_ : (NTT_P_SCRATCH32 ? 1 : MEMW_);
+  static constexpr int TW = 2;  // Shoup pair (w, floor(w 2^32 / p))
+  static constexpr int LDSW = 1;
+  static constexpr int IN = 4;       // bound hints of the generic kernels (every value here is < 2p)
   static constexpr int MUL_OUT = 4;
   static constexpr int EPT = 8;
-  // 1-limb P path (8-B `long long` in HBM, 4-B words in LDS): 8192-element tiles (32 KiB LDS,
-  // 1024 threads) and >= 16 columns per column-pass workgroup, so every HBM run is >= 128 B;
-  // 2048-element tiles left 64-B runs at radix 256 and 32-B runs at radix 512 (2.0-3.3 TB/s).
-  static constexpr int TILE_LOG = (N == 1) ? NTT_TILE_LOG_P : ((N <= 9) ? 11 : 10);
-  static constexpr int MIN_COLS_LOG = (N == 1) ? NTT_MIN_COLS_LOG_P : 2;
-  // HBM-bound at 1 limb: pass 1 takes its outer twiddles from the two-level tables (2 cheap
-  // products) instead of streaming an n-entry table (+50 % pass-1 traffic)
-  static constexpr bool PASS1_FULL_TABLE = (N == 1) ? NTT_P_PASS1_TABLE : true;
+  // 8192-element tiles (32 KiB LDS, 1024 threads) and >= 16 columns per column-pass workgroup, so
+  // every HBM run is >= 128 B; 2048-element tiles left 64-B runs at radix 256 and 32-B runs at
+  // radix 512 (2.0-3.3 TB/s).
+  static constexpr int TILE_LOG = NTT_TILE_LOG_P;
+  static constexpr int MIN_COLS_LOG = NTT_MIN_COLS_LOG_P;
+  // pass 1 takes its outer twiddles from the two-level tables (two cheap products) instead of
+  // streaming an n-entry table (+50 % pass-1 traffic)
+  static constexpr bool PASS1_FULL_TABLE = NTT_P_PASS1_TABLE;
   static constexpr bool SHOUP_OUTER = false;
   // the parallel-load stage (parallel-load.cu:114-193, re-derived): the pass's w_R^e table (R <= 512
-  // words) is staged into LDS while the tile's HBM loads are in flight; sub-stages read twiddles
-  // from LDS instead of issuing L1/L2 loads beside the data stream
-  static constexpr bool LDS_TW = (N == 1) && NTT_P_LDS_TW;
+  // Shoup pairs) is staged into LDS while the tile's HBM loads are in flight; sub-stages read their
+  // twiddles from LDS instead of issuing L1/L2 loads beside the data stream
+  static constexpr bool LDS_TW = NTT_P_LDS_TW;
   static constexpr int WAVES_PER_EU = 4;
   static constexpr bool LDS_SPLIT = false;
+  static constexpr bool FASTRED = false;
   struct Tw {
-    uint32_t w[N];  // w R mod p
+    uint32_t w[1];  // canonical w
+    uint32_t ws;    // floor(w 2^32 / p)
   };
   struct Args {
-    Modulus<N> M;
-    Tw w8[3];
-    Tw ninv;
+    uint32_t p, p2;  // p, 2p
+    uint32_t pinv;   // p^-1 mod 2^32 (Montgomery products)
+    Tw w8[3];        // w_8^1, w_8^2, w_8^3
+    Tw ninv;         // n^-1
   };
+  __device__ static __forceinline__ uint32_t red(uint32_t x, uint32_t m) {  // x < 2m -> x < m
+    return min(x, x - m);
+  }
+  __device__ static __forceinline__ uint32_t shoup(uint32_t x, uint32_t w, uint32_t ws, uint32_t p) {
+    const uint32_t q = __umulhi(x, ws);
+    return x * w - q * p;  // [0, 2p)
+  }
   template <int MW = MEMW_>
   __device__ static __forceinline__ void load(uint32_t (&x)[W], const uint32_t* __restrict__ base, size_t idx) {
     static_assert(MW == MEMW_ || MW == SCRW, "HBM width");
-    if constexpr (N == 1 && MW == 1) {
+    if constexpr (MW == 1)
       x[0] = base[idx];
-    } else if constexpr (N == 1) {
+    else
       x[0] = reinterpret_cast<const uint2*>(base)[idx].x;
-    } else {
-      const uint4* p = reinterpret_cast<const uint4*>(base + idx * MEMW);
-#pragma unroll
-      for (int q = 0; q < N / 4; ++q) {
-        const uint4 v = p[q];
-        x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
-      }
-    }
   }
-  static constexpr bool FASTRED = false;
   template <int FROM, int TO, bool FAST = false, bool R32 = true>
-  __device__ static __forceinline__ void reduce(uint32_t (&)[W], const Args&) {}
+  __device__ static __forceinline__ void reduce(uint32_t (&)[W], const Args&) {}  // always < 2p
+  template <int MW = MEMW_>
+  __device__ static __forceinline__ void put(uint32_t* __restrict__ base, size_t idx, uint32_t v) {
+    static_assert(MW == MEMW_ || MW == SCRW, "HBM width");
+    if constexpr (MW == 1)
+      base[idx] = v;
+    else
+      reinterpret_cast<uint2*>(base)[idx] = make_uint2(v, 0u);
+  }
+  // scratch between passes: the lazy value (< 2p < 2^31)
   template <int BOUND, bool FAST = false, int MW = MEMW_, bool WT = false>
   __device__ static __forceinline__ void store_lazy(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
-                                                    const Args& A) {
+                                                    const Args&) {
     static_assert(!WT, "write-through scratch stores: Eng29 engines only (fused schedule)");
-    store<BOUND, FAST, MW>(base, idx, x, A);
+    put<MW>(base, idx, x[0]);
   }
+  // canonical (< p)
   template <int BOUND, bool FAST = false, int MW = MEMW_>
   __device__ static __forceinline__ void store(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
-                                               const Args&) {
-    static_assert(MW == MEMW_ || MW == SCRW, "HBM width");
-    if constexpr (N == 1 && MW == 1) {
-      base[idx] = x[0];
-    } else if constexpr (N == 1) {
-      reinterpret_cast<uint2*>(base)[idx] = make_uint2(x[0], 0u);
-    } else {
-      uint4* p = reinterpret_cast<uint4*>(base + idx * MEMW);
-#pragma unroll
-      for (int q = 0; q < N / 4; ++q) p[q] = make_uint4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
-    }
+                                               const Args& A) {
+    put<MW>(base, idx, red(x[0], A.p));
   }
   __device__ static __forceinline__ void tload(Tw& t, const uint32_t* __restrict__ tab, size_t idx) {
-#pragma unroll
-    for (int i = 0; i < N; ++i) t.w[i] = tab[idx * N + i];
+    const uint2 v = reinterpret_cast<const uint2*>(tab)[idx];
+    t.w[0] = v.x;
+    t.ws = v.y;
+  }
+  __device__ static __forceinline__ void tload_lds(Tw& t, const uint32_t* lds_tw, uint32_t idx) {
+    const uint2 v = reinterpret_cast<const uint2*>(lds_tw)[idx];
+    t.w[0] = v.x;
+    t.ws = v.y;
   }
   __device__ static __forceinline__ void mul(uint32_t (&x)[W], const Tw& t, const Args& A) {
-    mont_mul<N>(x, x, t.w, A.M);
+    x[0] = shoup(x[0], t.w[0], t.ws, A.p);
   }
+  __device__ static __forceinline__ void mul_u(uint32_t (&x)[W], const Tw& t, const Args& A) { mul(x, t, A); }
+  // x y / 2^32 mod p in (0, 2p) for x y < 2^32 p (x, y < 2p: 4p^2 < 2^32 p)
   __device__ static __forceinline__ void mulv(uint32_t (&x)[W], const uint32_t (&y)[W], const Args& A) {
-    mont_mul<N>(x, x, y, A.M);
+    const uint32_t lo = x[0] * y[0], hi = __umulhi(x[0], y[0]);
+    const uint32_t m = lo * A.pinv;
+    x[0] = hi - __umulhi(m, A.p) + A.p;
   }
+  // lazy DIF butterfly: a, b < 2p -> (a + b, a - b), both reduced to < 2p
   template <int K>
   __device__ static __forceinline__ void bfly_l(uint32_t (&a)[W], uint32_t (&b)[W], const Args& A) {
-    uint32_t s[W], d[W];
-    add_mod<N>(s, a, b, A.M);
-    sub_mod<N>(d, a, b, A.M);
-#pragma unroll
-    for (int i = 0; i < W; ++i) { a[i] = s[i]; b[i] = d[i]; }
+    const uint32_t s = a[0] + b[0], d = a[0] - b[0] + A.p2;
+    a[0] = red(s, A.p2);
+    b[0] = red(d, A.p2);
   }
   template <int K>
-  __device__ static __forceinline__ void bfly_w_l(uint32_t (&a)[W], uint32_t (&b)[W], const Tw& t,
-                                                  const Args& A) {
-    bfly_l<K>(a, b, A);
-    mont_mul<N>(b, b, t.w, A.M);
+  __device__ static __forceinline__ void bfly_w_l(uint32_t (&a)[W], uint32_t (&b)[W], const Tw& t, const Args& A) {
+    const uint32_t s = a[0] + b[0], d = a[0] - b[0] + A.p2;  // d < 4p: any 32-bit x is fine for Shoup
+    a[0] = red(s, A.p2);
+    b[0] = shoup(d, t.w[0], t.ws, A.p);
   }
 };
 

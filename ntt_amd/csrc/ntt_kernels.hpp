@@ -68,7 +68,8 @@ struct PassArgs {
   uint32_t mid_bits[4];  // final pass: middle digit widths, least significant (k_{p-1}) first
   uint32_t mid_off[4];   // final pass: output bit offset (relative to R_1) of those digits
   uint32_t flags;        // bit 0: multiply outputs by ninv (single-pass inverse); bit 1: final pass
-                         // writes each output to its input's position (NTT_PLAN_IN_PLACE)
+                         // writes each output to its input's position (NTT_PLAN_IN_PLACE); bit 2:
+                         // XCD-grouped tile order (tiles t and t + 1 on one XCD, k_pass)
   uint32_t src_user;     // column pass: src is the caller's buffer (E::MEMW words/element), not scratch (E::SCRW)
   size_t batch_stride;   // 32-bit words between batched transforms in the caller's buffers (n * E::MEMW)
   // ---- distributed four-step addressing (ntt_rplan_*); fs == 0: plain batched transforms.
@@ -87,6 +88,11 @@ struct PassArgs {
                            // E::SCRW words; index b N + k in Mode B, k 2^il + b in Mode I) or null
   uint32_t tw_sh;          // column pass: tw_full holds Shoup pairs (canonical w, floor(w B / p); E::TW words
                            // per entry, E::SHOUP_OUTER engines) instead of w R_e in the element format
+  // ---- in-place final pass with the digit reversal fused (k_final_ipn, NTT_PLAN_IN_PLACE):
+  uint32_t* ipn_sync;        // [0] tile ticket, [1] workgroups exited, [2] watchdog; slab m: reads done at
+                             // [32 (1 + m)], ready at [32 (1 + m) + 1] (one 128-B line per slab)
+  const uint32_t* ipn_order; // slab (middle-digit value) of the i-th slab in ticket order (pairs adjacent)
+  uint32_t ipn_strips;       // workgroups per slab (R_1 / T)
 };
 enum : uint32_t { FS_MAP_IN = 1u, FS_MAP_OUT = 2u, FS_IL = 4u };
 
@@ -95,7 +101,7 @@ enum : uint32_t { FS_MAP_IN = 1u, FS_MAP_OUT = 2u, FS_IL = 4u };
 // workgroups through counters instead of kernel boundaries.  Word layout of `sync` (zero before the
 // first launch; the last workgroup to leave re-zeroes it): [0] tile ticket, [1] workgroups exited,
 // [2] watchdog (non-zero: a dependency wait gave up), [3] spare, [4, 4 + n12) pass 1 -> 2 counters,
-// [4 + n12, 4 + n12 + n23) pass 2 -> final counters.
+// [4 + n12, 4 + n12 + n23) pass 2 -> final counters, then one ready word per counter (rbase).
 struct FusedArgs {
   uint32_t* sync;
   uint32_t tiles;      // tiles per pass (n / TILE)
@@ -107,6 +113,9 @@ struct FusedArgs {
   uint32_t r2;                 // final tile w: waits on counter n12 + (w >> r2)
   uint32_t n12, n23;
   uint32_t need12, need23;     // arrivals per counter
+  uint32_t rbase;              // ready word of counter i at sync[rbase + 32 i] (one 128-B line each)
+  uint32_t dbg;                // diagnostics only (NTT_FUSED_DBG): bit 0 no dependency waits (wrong
+                               // output), bit 2 static tile order (needs every workgroup resident)
 };
 template <class E>
 hipError_t launch_fused3(int r1, int r2, int r3, const uint32_t* src, uint32_t* scratch, uint32_t* dst,
@@ -115,6 +124,11 @@ hipError_t launch_fused3(int r1, int r2, int r3, const uint32_t* src, uint32_t* 
 // workgroups one launch of k_fused3<E, r1, r2, r3> keeps resident on `device` (occupancy query x CUs)
 template <class E>
 hipError_t fused3_capacity(int r1, int r2, int r3, int device, uint32_t* wgs);
+
+// The in-place final pass with the digit reversal fused (NTT_PLAN_IN_PLACE, batch 1): A.ipn_* set,
+// grid = n / TILE workgroups, src == dst.  See k_final_ipn.
+template <class E>
+hipError_t launch_final_ipn(int logr, uint32_t* data, const PassArgs<E>& A, uint32_t grid, hipStream_t st);
 
 template <class E, int KIND>
 hipError_t launch_pass_kind(int logr, const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t grid,

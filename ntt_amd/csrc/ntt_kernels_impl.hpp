@@ -157,12 +157,12 @@ __device__ __forceinline__ void twiddle_mul(uint32_t (&x)[E::W], const uint32_t*
   E::tload(w, tab, e);
   E::mul(x, w, F);
 }
-// the same from the LDS copy of the table (E::LDS_TW engines: one word per entry)
+// the same from the LDS copy of the table (E::LDS_TW engines: E::TW words per entry)
 template <class E>
 __device__ __forceinline__ void twiddle_mul_lds(uint32_t (&x)[E::W], const uint32_t* lds_tw, uint32_t e,
                                                 const typename E::Args& F) {
   typename E::Tw w;
-  w.w[0] = lds_tw[e];
+  E::tload_lds(w, lds_tw, e);
   E::mul(x, w, F);
 }
 
@@ -305,6 +305,39 @@ enum : int { PRO_NONE = 0, PRO_PW = 1, PRO_COSET = 2 };
 #ifndef NTT_COL_R32_BELOW
 #define NTT_COL_R32_BELOW 8
 #endif
+// ---- in-place final pass with the digit reversal fused (NTT_PLAN_IN_PLACE; k_final_ipn below).
+// The final pass's outputs of slab `mid` belong in slab `midrev` (the palindromic schedule makes the
+// digit reversal an involution), so a tile may store only after every tile of slab midrev has READ
+// its elements (an anti-dependency: nothing handed-off is loaded, so no acquire is needed).  Reads
+// are counted per slab; the slab's last reader raises the slab's ready word.  Slab m's two words live
+// on a 128-B line of their own (ipn_sync[32 (1 + m)]), the ticket / exit / watchdog words on line 0.
+template <class E>
+__device__ __forceinline__ void ipn_signal_read(const PassArgs<E>& A, uint32_t mid) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's loads have returned
+  __syncthreads();
+  uint32_t* line = A.ipn_sync + 32 * (1 + mid);  // [0] reads done, [1] ready
+  if (threadIdx.x == 0 && __hip_atomic_fetch_add(line, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == A.ipn_strips - 1)
+    __hip_atomic_store(line + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class E>
+__device__ __forceinline__ void ipn_wait_mirror(const PassArgs<E>& A, uint32_t midrev) {
+  if (threadIdx.x == 0) {
+    uint32_t* ready = A.ipn_sync + 32 * (1 + midrev) + 1;
+    for (uint32_t spins = 0;; ++spins) {
+      uint32_t v = 1u;
+      __hip_atomic_compare_exchange_strong(ready, &v, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v) break;
+      if (spins < 8) __builtin_amdgcn_s_sleep(4);
+      else __builtin_amdgcn_s_sleep(32);
+      if (spins == (1u << 21)) {  // ~2 s: give up (watchdog word; the output is then wrong)
+        __hip_atomic_store(A.ipn_sync + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
 // LDS of one pass tile (words), and whether the pass stages its w_R^e table in LDS: E::LDS_TW
 // (parallel-load stage), not in a first pass with two-level outer twiddles (the P path's pass 1),
 // where it measured slower (profiles/r02_ldstw/)
@@ -322,14 +355,17 @@ __host__ __device__ constexpr bool pass_ltw() {
 }
 
 // One workgroup tile of one pass: tile w (the workgroup index of a k_pass launch) of transform bq
-// (its blockIdx.y).  lds: pass_lds_words() words, lds_tw: 2^LOGR words when pass_ltw().  k_pass runs
+// (its blockIdx.y).  lds: pass_lds_words() words, lds_tw: 2^LOGR E::TW words when pass_ltw().  k_pass runs
 // one tile per workgroup; the fused single-launch schedule (k_fused3) runs several passes' tiles
 // in one persistent workgroup.
 // LOOPED (persistent workgroups, k_fused3): the thread index is re-read per tile through an opaque
 // copy, so that the compiler does not hoist every lane-dependent address out of the tile loop (held in
 // VGPRs across the whole loop, they spilled 200-380 B per thread; per tile they cost a few VALU ops).
+// IPN (final pass of an in-place plan, k_final_ipn): outputs go to their natural positions in the same
+// buffer; a tile's loads are counted in per slab, and its stores wait until the mirror slab has been
+// read (see k_final_ipn).
 template <class E, int LOGR, int KIND, bool FULLTW, bool FAST, int PRO = PRO_NONE, bool SRC_USER = true,
-          int FSM = 0, bool SHTW = false, bool WT = false, bool LOOPED = false>
+          int FSM = 0, bool SHTW = false, bool WT = false, bool LOOPED = false, bool IPN = false>
 __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                           const PassArgs<E>& A, const uint32_t w, const uint32_t bq,
                                           uint32_t* __restrict__ lds, uint32_t* __restrict__ lds_tw) {
@@ -427,11 +463,12 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
   // ------------------------------------------------------------------ sub-stage 0: global -> regs
   // E::LDS_TW: this pass's w_R^e words, loaded ahead of the tile (L2 hits) and stored to LDS after
   // sub-stage 0 (which still multiplies from the global table)
-  uint32_t stw[LTW ? ((1 << LOGR) + NT - 1) / NT : 1];
+  constexpr int TWWORDS = LTW ? (1 << LOGR) * E::TW : 1;  // the staged table, E::TW words per entry
+  uint32_t stw[LTW ? (TWWORDS + NT - 1) / NT : 1];
   if constexpr (LTW && S::nsub > 1) {
-    static_for<((1 << LOGR) + NT - 1) / NT>([&](auto I) {
+    static_for<(TWWORDS + NT - 1) / NT>([&](auto I) {
       constexpr int i = I;
-      stw[i] = (t + NT * i < (1 << LOGR)) ? A.tw_int[t + NT * i] : 0u;
+      stw[i] = (t + NT * i < TWWORDS) ? A.tw_int[t + NT * i] : 0u;
     });
   }
   {
@@ -503,12 +540,14 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
     if constexpr (LTW && S::nsub > 1) {
       // parallel-load stage: the table words loaded with the tile (above) go to LDS now; the first
       // exchange's barrier publishes them to sub-stages 1.. (no barrier of its own)
-      static_for<((1 << LOGR) + NT - 1) / NT>([&](auto I) {
+      static_for<(TWWORDS + NT - 1) / NT>([&](auto I) {
         constexpr int i = I;
-        if (t + NT * i < (1 << LOGR)) lds_tw[t + NT * i] = stw[i];
+        if (t + NT * i < TWWORDS) lds_tw[t + NT * i] = stw[i];
       });
     }
   }
+
+  if constexpr (IPN) ipn_signal_read(A, mid);  // this tile's elements are in registers now
 
   // ------------------------------------------------------------------ sub-stages 1..nsub-1 via LDS
   if constexpr (S::nsub > 1) substage<E, LOGR, T, TE, NT, 1, FAST, R32, LTW>(x, cl, pil, lds, A, t, lds_tw, w);
@@ -519,6 +558,7 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
   static_assert(S::nsub <= 6, "sub-stages");
 
   // ------------------------------------------------------------------ output
+  if constexpr (IPN) ipn_wait_mirror(A, midrev);  // the slab this tile writes into has been read
   {
     constexpr int ls = S::nsub - 1;
     constexpr int qb = S::qb(ls), Q = 1 << qb, G = EPT / Q, sb = S::logsig(ls), lN = S::logN(ls);
@@ -578,7 +618,7 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
           if (fs_il) {
             const uint32_t k1 = k10 + (c >> tb_log), b = b0 + (c & ((1u << tb_log) - 1));
             pos = (((size_t)k1 + ((size_t)midrev << A.r1) + ((size_t)kn << (A.log_n - LOGR))) << A.il) + b;
-          } else if (A.flags & 2u) {  // NTT_PLAN_IN_PLACE: the input's own position; k_digitrev_swap follows
+          } else if (!IPN && (A.flags & 2u)) {  // NTT_PLAN_IN_PLACE: the input's own position; k_digitrev_swap follows
             pos = ((size_t)(k10 + c) << (A.log_n - A.r1)) + ((size_t)mid << LOGR) + kn;
           } else {
             pos = (size_t)(k10 + c) + ((size_t)midrev << A.r1) + ((size_t)kn << (A.log_n - LOGR));
@@ -616,8 +656,83 @@ template <class E, int LOGR, int KIND, bool FULLTW, bool FAST, int PRO = PRO_NON
 __global__ __launch_bounds__((1 << E::TILE_LOG) / E::EPT) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
 void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, const PassArgs<E> A) {
   __shared__ __attribute__((aligned(16))) uint32_t lds[pass_lds_words<E, LOGR, KIND>()];
-  __shared__ uint32_t lds_tw[pass_ltw<E, KIND, FULLTW>() ? (1 << LOGR) : 1];
-  pass_tile<E, LOGR, KIND, FULLTW, FAST, PRO, SRC_USER, FSM, SHTW>(src, dst, A, blockIdx.x, blockIdx.y, lds, lds_tw);
+  __shared__ __attribute__((aligned(16))) uint32_t lds_tw[pass_ltw<E, KIND, FULLTW>() ? (1 << LOGR) * E::TW : 1];
+  // flags bit 2: workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share one, for speed
+  // only), so tile (b mod 8) G/8 + b / 8 puts neighbouring tiles -- which share 128-B lines when a
+  // pass's runs are 64 B -- on one XCD's L2 at about the same time
+  uint32_t w = blockIdx.x;
+  if (A.flags & 4u) {
+    const uint32_t G = gridDim.x;
+    if ((G & 7u) == 0) w = (w & 7u) * (G >> 3) + (w >> 3);
+  }
+  pass_tile<E, LOGR, KIND, FULLTW, FAST, PRO, SRC_USER, FSM, SHTW>(src, dst, A, w, blockIdx.y, lds, lds_tw);
+}
+
+// In-place final pass with the fused digit reversal: one tile per workgroup, tiles taken from a
+// ticket counter in slab-pair order (slab m's tiles, then slab rev(m)'s), so that a tile waits only
+// for tiles of its own pair.  Deadlock-free at any residency: every ticket below the newest pair's
+// was taken by a running workgroup, those pairs complete, and a pair has 2 R_1 / T <= 128 tiles.
+// The last workgroup out re-zeroes the counters for the next launch.
+template <class E, int LOGR>
+__global__ __launch_bounds__((1 << E::TILE_LOG) / E::EPT) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
+void k_final_ipn(uint32_t* data, const PassArgs<E> A) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[pass_lds_words<E, LOGR, KIND_FINAL>()];
+  __shared__ __attribute__((aligned(16))) uint32_t lds_tw[pass_ltw<E, KIND_FINAL, false>() ? (1 << LOGR) * E::TW : 1];
+  __shared__ uint32_t s_w, s_last;
+  const uint32_t t = threadIdx.x;
+  if (t == 0) {
+    const uint32_t tk = __hip_atomic_fetch_add(A.ipn_sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t slab = A.ipn_order[tk / A.ipn_strips], strip = tk % A.ipn_strips;
+    s_w = (strip << (A.log_n - A.r1 - LOGR)) | slab;  // the final pass's tile index: (k1 group, mid)
+  }
+  __syncthreads();
+  const uint32_t w = s_w;
+  if constexpr (E::FASTRED) {
+    if (A.F.red_ok)
+      pass_tile<E, LOGR, KIND_FINAL, false, true, PRO_NONE, true, 0, false, false, false, true>(data, data, A, w, 0, lds,
+                                                                                              lds_tw);
+    else
+      pass_tile<E, LOGR, KIND_FINAL, false, false, PRO_NONE, true, 0, false, false, false, true>(data, data, A, w, 0,
+                                                                                               lds, lds_tw);
+  } else {
+    pass_tile<E, LOGR, KIND_FINAL, false, false, PRO_NONE, true, 0, false, false, false, true>(data, data, A, w, 0, lds,
+                                                                                             lds_tw);
+  }
+  if (t == 0)
+    s_last = __hip_atomic_fetch_add(A.ipn_sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (s_last) {  // nobody touches the counters again in this launch
+    const uint32_t slabs = (uint32_t)(gridDim.x / A.ipn_strips);
+    for (uint32_t m = t; m < slabs; m += blockDim.x) {
+      A.ipn_sync[32 * (1 + m)] = 0u;
+      A.ipn_sync[32 * (1 + m) + 1] = 0u;
+    }
+    if (t == 0) A.ipn_sync[0] = A.ipn_sync[1] = 0u;
+  }
+}
+
+template <class E>
+hipError_t launch_final_ipn(int logr, uint32_t* data, const PassArgs<E>& A, uint32_t grid, hipStream_t st) {
+  constexpr int TL = tile_log_of<E>();
+  constexpr int NT = (1 << TL) / E::EPT;
+  switch (logr) {
+#define NTT_IPN_CASE(R)                                                                          \
+  case R:                                                                                        \
+    if constexpr (R <= TL - E::MIN_COLS_LOG) {                                                   \
+      hipLaunchKernelGGL((k_final_ipn<E, R>), dim3(grid), dim3(NT), 0, st, data, A);             \
+      return hipGetLastError();                                                                  \
+    }                                                                                            \
+    return hipErrorInvalidValue;
+    NTT_IPN_CASE(3)
+    NTT_IPN_CASE(4)
+    NTT_IPN_CASE(5)
+    NTT_IPN_CASE(6)
+    NTT_IPN_CASE(7)
+    NTT_IPN_CASE(8)
+    NTT_IPN_CASE(9)
+#undef NTT_IPN_CASE
+    default: return hipErrorInvalidValue;
+  }
 }
 
 // ---------------------------------------------------------------------------- fused 3-pass launch
@@ -635,20 +750,37 @@ void k_pass(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, const 
 // by running workgroups whose own waits are on smaller tickets still (pass 1 waits on nothing).
 // Hand-off (MI355X_MICROARCH.md § visibility, publish form R1): scratch stores are write-through
 // (sc1), every wave drains them (s_waitcnt vmcnt(0)), a workgroup barrier, then one lane's agent-scope
-// counter add; the consumer polls relaxed, takes ONE agent-scope acquire, waits, barrier, plain loads.
+// counter add; the group's last arrival raises a ready word; the consumer polls it, takes ONE
+// agent-scope acquire, waits, barrier, plain loads.
 // Every dependency wait is bounded (watchdog word, then the tile runs anyway: wrong output, no hang),
 // so every wave reaches the exit; the last workgroup out re-zeroes the counters for the next launch.
-__device__ __forceinline__ void fused_publish(uint32_t* cnt) {
+// Producer: every wave drains its write-through stores, a barrier, then one lane counts the tile in;
+// the group's last arrival (told by the value its add returns) raises the group's ready word, which
+// lies on a 128-B line of its own.  Consumers poll only that word: 128 pollers on the counter itself
+// queued the producers' adds behind their polls (2^20: 350-450 us per transform instead of 160).
+__device__ __forceinline__ void fused_publish(uint32_t* cnt, uint32_t* ready, uint32_t need) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave: its write-through stores are done
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0 && __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == need - 1)
+    __hip_atomic_store(ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void fused_wait(uint32_t* cnt, uint32_t need, uint32_t* watchdog) {
+// Consumer: one lane polls the ready word (an atomic compare-exchange, performed where the atomic
+// store landed), sleeping 60 ns .. 1 us between polls; then ONE agent-scope acquire, its wait, and
+// the workgroup barrier before any load of the handed-off tile.  Bounded: after ~2 s it gives up and
+// raises the watchdog word (the output is then wrong; every wave still reaches the exit).
+__device__ __forceinline__ void fused_wait(uint32_t* ready, uint32_t* watchdog, uint32_t dbg) {
+  if (dbg & 1u) return;  // diagnostics only: no dependency waits (wrong output)
   if (threadIdx.x == 0) {
     uint32_t spins = 0;
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins == (1u << 24)) {  // ~1 s: give up (reported through the watchdog word)
+    for (;;) {
+      uint32_t v = 1u;
+      __hip_atomic_compare_exchange_strong(ready, &v, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      if (v) break;
+      if (spins < 4) __builtin_amdgcn_s_sleep(2);
+      else if (spins < 16) __builtin_amdgcn_s_sleep(8);
+      else __builtin_amdgcn_s_sleep(32);
+      if (++spins == (1u << 21)) {
         __hip_atomic_store(watchdog, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
@@ -692,48 +824,57 @@ void k_fused3(const FusedKArgs<E> K) {
   uint32_t* const cnt12 = F.sync + 4;
   uint32_t* const cnt23 = F.sync + 4 + F.n12;
   const uint32_t t = threadIdx.x, total = 3 * F.tiles;
-  if (t == 0) s_ticket = __hip_atomic_fetch_add(F.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  uint32_t tk = s_ticket;
-  // the next ticket: its add is issued before the tile, its value used after it
+  // Tile order: every tile is a ticket sync[0]++, the first taken at start, each later one while the
+  // previous tile's stores drain, i.e. in completion order.  (A ticket prefetched at tile START let
+  // the first workgroups to start take two or three pass-1 tiles each while later ones idled on
+  // pass-2 tiles: 4x slower at 2^20.)
+  uint32_t stat = blockIdx.x;  // dbg bit 2: static order b, b + nwg, ...
   auto ticket = [&]() -> uint32_t {
+    if (F.dbg & 4u) return stat += F.nwg;
     return t == 0 ? __hip_atomic_fetch_add(F.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
   };
+  if (t == 0) s_ticket = (F.dbg & 4u) ? blockIdx.x : ticket();
+  __syncthreads();
+  uint32_t tk = s_ticket;
   auto advance = [&](uint32_t next) {
     __syncthreads();  // every wave is done with this tile's LDS and s_ticket
     if (t == 0) s_ticket = next;
     __syncthreads();
     tk = s_ticket;
   };
-  // tickets are handed out in pass-major order, so a workgroup's tickets only grow: one loop per pass
+  // tickets only grow per workgroup and are handed out pass-major: one loop per pass
   while (tk < F.tiles) {  // pass 1: the caller's buffer -> scratch
-    const uint32_t next = ticket(), w = tk;
+    const uint32_t w = tk;
     const FusedKArgs<E>& L = fused_kargs<E>();
     pass_tile<E, R1, KIND_COLUMN, true, true, PRO_NONE, true, 0, false, true, true>(L.src, L.scratch, L.A1, w, 0,
                                                                                       lds, lds_tw);
-    fused_publish(cnt12 + ((w & F.k1_mask) >> F.k1_shift));
+    const uint32_t next = ticket();  // issued before the drain of this tile's stores
+    const uint32_t key = (w & F.k1_mask) >> F.k1_shift;
+    fused_publish(cnt12 + key, F.sync + F.rbase + 32 * key, F.need12);
     advance(next);
   }
   while (tk < 2 * F.tiles) {  // pass 2: scratch in place (Shoup-pair outer twiddles)
-    const uint32_t next = ticket(), w = tk - F.tiles, g = w & ((1u << F.cg_log) - 1);
-    fused_wait(cnt12 + (g >> F.k2_shift), F.need12, F.sync + 2);
+    const uint32_t w = tk - F.tiles, g = w & ((1u << F.cg_log) - 1);
+    fused_wait(F.sync + F.rbase + 32 * (g >> F.k2_shift), F.sync + 2, F.dbg);
     const FusedKArgs<E>& L = fused_kargs<E>();
     pass_tile<E, R2, KIND_COLUMN, true, true, PRO_NONE, true, 0, true, true, true>(L.scratch, L.scratch, L.A2, w, 0,
                                                                                      lds, lds_tw);
-    fused_publish(cnt23 + ((w >> F.cg_log) >> F.t3_log));
+    const uint32_t next = ticket();
+    const uint32_t key = (w >> F.cg_log) >> F.t3_log;
+    fused_publish(cnt23 + key, F.sync + F.rbase + 32 * (F.n12 + key), F.need23);
     advance(next);
   }
   while (tk < total) {  // final pass: scratch -> the caller's buffer, natural order
-    const uint32_t next = ticket(), w = tk - 2 * F.tiles;
-    fused_wait(cnt23 + (w >> F.r2), F.need23, F.sync + 2);
+    const uint32_t w = tk - 2 * F.tiles;
+    fused_wait(F.sync + F.rbase + 32 * (F.n12 + (w >> F.r2)), F.sync + 2, F.dbg);
     const FusedKArgs<E>& L = fused_kargs<E>();
     pass_tile<E, R3, KIND_FINAL, false, true, PRO_NONE, true, 0, false, false, true>(L.scratch, L.dst, L.A3, w, 0,
                                                                                        lds, lds_tw);
-    advance(next);
+    advance(ticket());
   }
   if (t == 0 && __hip_atomic_fetch_add(F.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == F.nwg - 1) {
     // the last workgroup out: nobody touches the counters again in this launch
-    const uint32_t words = 4 + F.n12 + F.n23;
+    const uint32_t words = F.rbase + 32 * (F.n12 + F.n23);
     for (uint32_t i = 0; i < words; ++i)
       if (i != 2) __hip_atomic_store(F.sync + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -1492,6 +1633,7 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
   template hipError_t launch_transpose<E>(const uint32_t*, uint32_t*, uint32_t, uint32_t, uint32_t, uint64_t,     \
                                           hipStream_t);                                                            \
   template hipError_t launch_digitrev_swap<E>(uint32_t*, const DrevArgs&, uint32_t, hipStream_t);                  \
+  template hipError_t launch_final_ipn<E>(int, uint32_t*, const PassArgs<E>&, uint32_t, hipStream_t);              \
   template hipError_t launch_pointwise<E>(const uint32_t*, const uint32_t*, uint32_t*, size_t,                     \
                                           const typename E::Args&, const uint32_t*, hipStream_t);                  \
   template hipError_t launch_build_tw<E>(uint32_t*, size_t, uint32_t, uint32_t, uint32_t, const uint32_t*,        \

@@ -144,10 +144,30 @@ static bool schedule_ok(const unsigned* r, unsigned p, unsigned tile_log) {
 }
 // narrow_first (HBM-bound engines): pass 1, whose columns are n / R_1 elements apart, takes a radix
 // one below the rest so that its workgroups read twice as wide runs (2^24 P: 7+8+9 instead of 8+8+8).
+// NTT_SCHEDULE="r1,r2,..." (experiments only): that radix sequence for the sizes it sums to, when the
+// pass kernels accept it.
+static bool schedule_env(unsigned log_n, unsigned tile_log, unsigned rmax, unsigned* r, unsigned& p) {
+  const char* v = getenv("NTT_SCHEDULE");
+  if (!v || !*v) return false;
+  unsigned rr[8], pp = 0, sum = 0;
+  for (const char* c = v; *c && pp < 8;) {
+    const unsigned x = (unsigned)strtoul(c, const_cast<char**>(&c), 10);
+    if (x < 3 || x > rmax) return false;
+    rr[pp++] = x;
+    sum += x;
+    if (*c == ',') ++c;
+    else if (*c) return false;
+  }
+  if (sum != log_n || pp < 2 || !schedule_ok(rr, pp, tile_log)) return false;
+  for (unsigned i = 0; i < pp; ++i) r[i] = rr[i];
+  p = pp;
+  return true;
+}
 static bool schedule(unsigned log_n, unsigned tile_log, unsigned min_cols_log, bool narrow_first, unsigned* r,
                      unsigned& p) {
   if (log_n <= 2) { p = 0; return true; }
   if (log_n <= tile_log) { p = 1; r[0] = log_n; return true; }
+  if (schedule_env(log_n, tile_log, tile_log - min_cols_log, r, p)) return true;
   const unsigned rmax = tile_log - min_cols_log;
   p = (log_n + rmax - 1) / rmax;
   if (p < 2) p = 2;
@@ -309,19 +329,32 @@ template <int N, int MEMW_, int SCR_>
 struct EngHost<Eng32<N, MEMW_, SCR_>> {
   static constexpr int NH = N;
   using EA = typename Eng32<N, MEMW_, SCR_>::Args;
+  using ET = typename Eng32<N, MEMW_, SCR_>::Tw;
   HostField<NH> const* H = nullptr;
   void init(const HostField<NH>& h) { H = &h; }
+  // canonical c -> Shoup pair (c, floor(c 2^32 / p))
   void encode(const Vec<NH>& c, uint32_t* out) const {
-    const Vec<NH> m = H->to_mont(c);
-    for (int i = 0; i < N; ++i) out[i] = m[i];
+    out[0] = c[0];
+    out[1] = (uint32_t)(((uint64_t)c[0] << 32) / H->M.p[0]);
   }
-  // Montgomery form c R is already the R_e-scaled value
-  void encode_scaled(const Vec<NH>& c, uint32_t* out) const { encode(c, out); }
-  bool check_modulus(const uint32_t* p) const { return p[NH - 1] < 0x7fffffffu; }
+  // entry whose value is c R_e (R_e = 2^32, the Montgomery radix of Eng32::mulv): c's Montgomery form
+  void encode_scaled(const Vec<NH>& c, uint32_t* out) const { encode(H->to_mont(c), out); }
+  // lazy values up to 4p must fit 32 bits
+  bool check_modulus(const uint32_t* p) const { return p[0] < (1u << 30); }
   void fill_args(EA& A, const uint32_t* p, const Vec<NH>* w8, const Vec<NH>& ninv) const {
-    A.M = H->M;
-    for (int k = 0; k < 3; ++k) encode(w8[k], A.w8[k].w);
-    encode(ninv, A.ninv.w);
+    A.p = p[0];
+    A.p2 = 2 * p[0];
+    uint32_t inv = 1;
+    for (int i = 0; i < 5; ++i) inv *= 2 - p[0] * inv;  // p^-1 mod 2^32 (Newton)
+    A.pinv = inv;
+    uint32_t t[2];
+    auto tw = [&](const Vec<NH>& c, ET& e) {
+      encode(c, t);
+      e.w[0] = t[0];
+      e.ws = t[1];
+    };
+    for (int k = 0; k < 3; ++k) tw(w8[k], A.w8[k]);
+    tw(ninv, A.ninv);
   }
 };
 
@@ -374,6 +407,7 @@ struct PlanImpl final : PlanBase {
     if (d_coset) hipFree(d_coset);
     if (d_coset_full) hipFree(d_coset_full);
     if (d_sync) hipFree(d_sync);
+    if (d_ipn) hipFree(d_ipn);
     for (auto& row : ev)
       for (auto& e : row)
         if (e) hipEventDestroy(e);
@@ -966,7 +1000,12 @@ struct PlanImpl final : PlanBase {
         A.tw_hi = d_tab + (inverse ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
         // pass 1 of a memory-bound engine (8-B P path) computes its outer twiddles from the
         // L2-resident two-level tables: two 32-bit products are cheaper than streaming an n-entry table
-        A.tw_full = (use_full && (i > 0 || E::PASS1_FULL_TABLE)) ? d_full + full_off[inverse ? 1 : 0][i] * SCRW : nullptr;
+        static const bool p1_full = [] {  // NTT_PASS1_FULL=1: pass 1 streams its table on every engine (A/B)
+          const char* v = getenv("NTT_PASS1_FULL");
+          return v && atoi(v) > 0;
+        }();
+        A.tw_full = (use_full && (i > 0 || E::PASS1_FULL_TABLE || p1_full)) ? d_full + full_off[inverse ? 1 : 0][i] * SCRW
+                                                                             : nullptr;
         if (i > 0 && d_full_sh && full_sh_ok[i]) {
           A.tw_full = d_full_sh + full_sh_off[inverse ? 1 : 0][i] * TW;
           A.tw_sh = 1;
@@ -1001,6 +1040,18 @@ struct PlanImpl final : PlanBase {
       set_fs(A, FS_MAP_OUT);
       if (io) A.tw_epi = static_cast<const uint32_t*>(io->tw_epi);
       if (inplace) A.flags |= 2u;
+      // XCD-grouped tile order (k_pass flag bit 2) for the column passes after the first whose runs are
+      // shorter than a 128-B line (the 8-B path's 4-B scratch at radix 512: 64-B runs), so that the
+      // two tiles sharing each line meet on one XCD's L2.  NTT_XCD_ORDER=0 off, =1 on every pass.
+      static const int xcd_order = [] {
+        const char* v = getenv("NTT_XCD_ORDER");
+        return v && *v ? atoi(v) : 2;
+      }();
+      if (!io && xcd_order > 0)
+        for (unsigned i = 0; i + 1 < npass; ++i) {
+          const unsigned run_bytes = (1u << (tile_log_of<E>() - r[i])) * SCRW * 4;
+          if (xcd_order == 1 || (i > 0 && run_bytes < 128)) PA[i].flags |= 4u;
+        }
       if constexpr (std::is_same_v<E, Eng256>) {  // the engine k_fused3 is instantiated for
         if (!io && !inplace && batch == 1 && fused_enabled() && fused_ready(PA)) {
           // one persistent launch for the three passes (NTT_PLAN_SINGLE_LAUNCH, k_fused3)
@@ -1014,7 +1065,16 @@ struct PlanImpl final : PlanBase {
         e = launch_pass<E>(KIND_COLUMN, (int)r[i], src, work, PA[i], grid, batch, st);
         mark(st);
       }
-      if (e == hipSuccess) {
+      if (e == hipSuccess && inplace && batch == 1 && ipn_ready(A)) {
+        // the final pass writes natural positions in place, the digit reversal fused (k_final_ipn)
+        PassArgs<E> B = A;
+        B.flags &= ~2u;
+        B.ipn_sync = d_ipn;
+        B.ipn_order = d_ipn + 32 * (1 + ipn_slabs);
+        B.ipn_strips = ipn_strips;
+        e = launch_final_ipn<E>((int)r[npass - 1], out, B, grid, st);
+        mark(st);
+      } else if (e == hipSuccess) {
         e = launch_pass<E>(KIND_FINAL, (int)r[npass - 1], work, out, A, grid, batch, st);
         mark(st);
         if (inplace && e == hipSuccess) {
@@ -1083,7 +1143,9 @@ struct PlanImpl final : PlanBase {
     F.n23 = 1u << (r1 - lt3);
     F.need12 = 1u << (lu - lt1 + r2);
     F.need23 = 1u << r2;
-    const size_t words = (4 + F.n12 + F.n23 + 3) & ~size_t(3);
+    if (const char* v = getenv("NTT_FUSED_DBG")) F.dbg = (uint32_t)atoi(v);
+    F.rbase = (4 + F.n12 + F.n23 + 31) & ~31u;
+    const size_t words = F.rbase + 32 * (F.n12 + F.n23);
     if (hipMalloc(&d_sync, words * 4) != hipSuccess) {
       d_sync = nullptr;
       return false;
@@ -1098,12 +1160,67 @@ struct PlanImpl final : PlanBase {
   // watchdog of the fused schedule: non-zero when a dependency wait gave up (then cleared)
   int device_status(unsigned* bad) override {
     *bad = 0;
-    if (!d_sync) return NTT_OK;
-    uint32_t w = 0;
-    if (hipMemcpy(&w, d_sync + 2, 4, hipMemcpyDeviceToHost) != hipSuccess) return NTT_ERR_HIP;
-    if (w && hipMemset(d_sync + 2, 0, 4) != hipSuccess) return NTT_ERR_HIP;
-    *bad = w;
+    for (uint32_t* d : {d_sync, d_ipn}) {
+      if (!d) continue;
+      uint32_t w = 0;
+      if (hipMemcpy(&w, d + 2, 4, hipMemcpyDeviceToHost) != hipSuccess) return NTT_ERR_HIP;
+      if (w && hipMemset(d + 2, 0, 4) != hipSuccess) return NTT_ERR_HIP;
+      *bad |= w;
+    }
     return NTT_OK;
+  }
+
+  // ---- in-place final pass with the fused digit reversal (NTT_PLAN_IN_PLACE, k_final_ipn)
+  uint32_t* d_ipn = nullptr;  // 32 (1 + slabs) sync words, then the slab order table
+  uint32_t ipn_slabs = 0, ipn_strips = 0;
+  bool ipn_built = false, ipn_ok = false;
+  // NTT_IPN=0 in the environment keeps the separate tile-swap pass (A/B)
+  bool ipn_ready(const PassArgs<E>& A) {
+    if (!ipn_built) {
+      ipn_built = true;
+      const char* v = getenv("NTT_IPN");
+      ipn_ok = !(v && v[0] == '0') && build_ipn(A);
+    }
+    return ipn_ok;
+  }
+  bool build_ipn(const PassArgs<E>& A) {
+    const unsigned tl = tile_log_of<E>(), rp = r[npass - 1];
+    if (npass < 2 || r[0] != rp || rp > 9 || tl < rp) return false;
+    const unsigned mid_log = log_n - r[0] - rp;
+    ipn_slabs = 1u << mid_log;
+    ipn_strips = 1u << (r[0] - (tl - rp));  // R_1 / T, T = TILE / R_p
+    if (r[0] < tl - rp || 2 * ipn_strips > 1024) return false;
+    // slab order: m, then its mirror (the final pass's middle-digit reversal, as k_pass computes it)
+    std::vector<uint32_t> order, seen(ipn_slabs, 0);
+    auto rev = [&](uint32_t m) {
+      uint32_t out = 0;
+      for (unsigned i = 0; i < A.nmid; ++i) {
+        out |= (m & ((1u << A.mid_bits[i]) - 1)) << A.mid_off[i];
+        m >>= A.mid_bits[i];
+      }
+      return out;
+    };
+    for (uint32_t m = 0; m < ipn_slabs; ++m) {
+      if (seen[m]) continue;
+      const uint32_t q = rev(m);
+      if (q >= ipn_slabs || rev(q) != m) return false;  // the schedule is not palindromic
+      order.push_back(m);
+      seen[m] = 1;
+      if (q != m) {
+        order.push_back(q);
+        seen[q] = 1;
+      }
+    }
+    const size_t sync_words = 32 * (1 + (size_t)ipn_slabs);
+    if (hipMalloc(&d_ipn, (sync_words + order.size()) * 4) != hipSuccess) {
+      d_ipn = nullptr;
+      return false;
+    }
+    if (hipMemset(d_ipn, 0, sync_words * 4) != hipSuccess ||
+        hipMemcpy(d_ipn + sync_words, order.data(), order.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess)
+      return false;
+    return true;
   }
 
   // ---- distributed four-step pieces (ntt_rplan, ntt_amd/csrc/ntt_rplan.cpp)

@@ -2,7 +2,7 @@
 # Single-launch (k_fused3) schedule: GPU tests, same-box A/B against the 3-launch schedule, rocprof.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/${TAG:-r03_fused}
+O=gpurun_out/${TAG:-r03_fused2}
 mkdir -p $O
 step() {  # name seconds cmd...
   local name=$1 t=$2; shift 2
