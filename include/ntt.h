@@ -207,6 +207,11 @@ int NTT_GZKP_256(uint32_t* data, uint32_t len, const void* reverse, uint32_t rev
 int NTT_GZKP_64(long long* data, const void* reverse, long long len, long long omega, int B, int G,
                 long long reverse_num);
 int ntt_last_error(void);
+/* The shims cache one plan per (modulus, generator, limbs, size, device) -- the reference rebuilt
+ * its tables on every call (GZKP-NTT.cu:1476-1500, big-num.cu:278-309) -- keeping at most
+ * NTT_SHIM_CACHE_PLANS (environment, default 8) and dropping the least recently used one beyond
+ * that.  This releases every cached plan (a shim call still running keeps its plan until it returns). */
+void ntt_shim_cache_clear(void);
 
 /* ---------------------------------------------------------------- one rank of the distributed four-step
  * New (the reference has no multi-GPU code).  The local steps of rank `rank` of `world`

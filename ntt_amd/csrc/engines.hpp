@@ -29,7 +29,7 @@
 #define NTT_P_NARROW_FIRST 1
 #endif
 #ifndef NTT_P_PASS1_TABLE
-#define NTT_P_PASS1_TABLE 0
+#define NTT_P_PASS1_TABLE 1
 #endif
 #ifndef NTT_P_LDS_TW
 #define NTT_P_LDS_TW 1
@@ -88,6 +88,7 @@ struct Eng29 {
   static constexpr bool LDS_SPLIT = false;
   static constexpr int MIN_COLS_LOG = 2;  // column passes own >= 4 adjacent columns: >= 128-B runs
   static constexpr bool PASS1_FULL_TABLE = NTT_256_PASS1_TABLE;  // VALU-bound: a table read beats a second product
+  static constexpr bool NARROW_FIRST = false;  // near-equal radices
   // column passes after the first take their outer twiddles as Shoup pairs (w, ws) from L2-resident
   // tables (E::TW words per entry): 143 MADs per product instead of the Montgomery product's 162
   static constexpr bool SHOUP_OUTER = (L == 9);
@@ -332,9 +333,13 @@ struct Eng32 {
   // radix 512 (2.0-3.3 TB/s).
   static constexpr int TILE_LOG = NTT_TILE_LOG_P;
   static constexpr int MIN_COLS_LOG = NTT_MIN_COLS_LOG_P;
-  // pass 1 takes its outer twiddles from the two-level tables (two cheap products) instead of
-  // streaming an n-entry table (+50 % pass-1 traffic)
+  // pass 1 streams its n-entry outer-twiddle table (4 B per entry: +33 % pass-1 bytes) instead of
+  // forming the twiddle from the two-level tables: those are 64 KiB + 64 KiB of Shoup pairs gathered
+  // per element, and the shorter arithmetic of this engine made pass 1 wait on them (2^26: 307 ->
+  // 237 us with the table, profiles/r03_pab/)
   static constexpr bool PASS1_FULL_TABLE = NTT_P_PASS1_TABLE;
+  // pass 1 (columns n / R_1 apart) takes a radix one below the rest: twice as wide runs (2^26: 8+9+9)
+  static constexpr bool NARROW_FIRST = NTT_P_NARROW_FIRST;
   static constexpr bool SHOUP_OUTER = false;
   // the parallel-load stage (parallel-load.cu:114-193, re-derived): the pass's w_R^e table (R <= 512
   // Shoup pairs) is staged into LDS while the tile's HBM loads are in flight; sub-stages read their

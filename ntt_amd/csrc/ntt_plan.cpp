@@ -369,8 +369,12 @@ struct PlanImpl final : PlanBase {
   typename E::Args Ff{}, Fi{};
   uint32_t* d_tab = nullptr;
   uint32_t* d_scratch = nullptr;
-  uint32_t* d_full = nullptr;  // per-pass outer twiddle tables (w R_e, HBM element format), both directions
-  size_t full_off[2][8] = {};  // element offsets into d_full, [dir][pass]
+  // per-pass outer twiddle tables (w R_e, HBM element format), one allocation per direction: the
+  // forward's at plan creation, the inverse's at the first inverse call (a forward-only user pays for
+  // one direction: 2^24 BN254 plan 1.55 -> 1.03 GB)
+  uint32_t* d_fulls[2] = {nullptr, nullptr};
+  size_t full_off[8] = {};  // element offsets of pass i's table in d_fulls[dir]
+  size_t full_elems = 0;    // entries per direction
   bool use_full = false;
   uint32_t* d_full_sh = nullptr;  // passes >= 2: the same tables as Shoup pairs (E::TW words per entry)
   size_t full_sh_off[2][8] = {};  // entry offsets into d_full_sh, [dir][pass]
@@ -397,7 +401,8 @@ struct PlanImpl final : PlanBase {
     hipSetDevice(device);
     if (d_tab) hipFree(d_tab);
     if (d_scratch) hipFree(d_scratch);
-    if (d_full) hipFree(d_full);
+    for (auto* p : d_fulls)
+      if (p) hipFree(p);
     if (d_full_sh) hipFree(d_full_sh);
     if (d_full_pm) hipFree(d_full_pm);
     if (d_stk_tab) hipFree(d_stk_tab);
@@ -506,7 +511,7 @@ struct PlanImpl final : PlanBase {
     }
 
     // ---- schedule + tables (engine-encoded)
-    if (!schedule(log_n, tile_log_of<E>(), E::MIN_COLS_LOG, !E::PASS1_FULL_TABLE && NTT_P_NARROW_FIRST, r, npass))
+    if (!schedule(log_n, tile_log_of<E>(), E::MIN_COLS_LOG, E::NARROW_FIRST, r, npass))
       return NTT_ERR_ARG;
     if (flags & NTT_PLAN_IN_PLACE) {
       // passes store their lazily reduced values where they read them: the scratch element must be
@@ -704,30 +709,36 @@ struct PlanImpl final : PlanBase {
     size_t elems = 0;
     unsigned blk = log_n;
     for (unsigned i = 0; i + 1 < npass; ++i) {
-      full_off[0][i] = elems;
+      full_off[i] = elems;
       elems += 1ull << blk;
       blk -= r[i];
     }
+    full_elems = elems;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return NTT_OK;
-    if (2 * elems * SCRW * 4 > free_b / 4) return NTT_OK;
-    if (hipMalloc(&d_full, 2 * elems * SCRW * 4) != hipSuccess) return NTT_ERR_HIP;
-    for (int dir = 0; dir < 2; ++dir) {
-      blk = log_n;
-      for (unsigned i = 0; i + 1 < npass; ++i) {
-        full_off[dir][i] = dir * elems + full_off[0][i];
-        const uint32_t* lo = d_tab + (dir ? off_los_i : off_los_f);
-        const uint32_t* hi = d_tab + (dir ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
-        // column-group-major layout of the pass kernel's tiles (T = TILE / R columns per workgroup)
-        if (launch_build_tw<E>(d_full + full_off[dir][i] * SCRW, 1ull << blk, r[i], tile_log_of<E>() - r[i],
-                               log_n - blk, lo, hi, lo_bits, dir ? Fi : Ff, nullptr) != hipSuccess)
-          return NTT_ERR_HIP;
-        blk -= r[i];
-      }
-    }
-    if (hipDeviceSynchronize() != hipSuccess) return NTT_ERR_HIP;
+    if (2 * elems * SCRW * 4 > free_b / 4) return NTT_OK;  // both directions within a quarter of free HBM
+    if (int rc = ensure_full(0)) return rc;
     use_full = true;
     return build_shoup_tables();
+  }
+  // the per-pass tables of one direction (the inverse's pass-1 table carries n^-1)
+  int ensure_full(int dir) {
+    if (d_fulls[dir]) return NTT_OK;
+    if (hipMalloc(&d_fulls[dir], full_elems * SCRW * 4) != hipSuccess) {
+      d_fulls[dir] = nullptr;
+      return NTT_ERR_HIP;
+    }
+    unsigned blk = log_n;
+    for (unsigned i = 0; i + 1 < npass; ++i) {
+      const uint32_t* lo = d_tab + (dir ? off_los_i : off_los_f);
+      const uint32_t* hi = d_tab + (dir ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
+      // column-group-major layout of the pass kernel's tiles (T = TILE / R columns per workgroup)
+      if (launch_build_tw<E>(d_fulls[dir] + full_off[i] * SCRW, 1ull << blk, r[i], tile_log_of<E>() - r[i], log_n - blk,
+                             lo, hi, lo_bits, dir ? Fi : Ff, nullptr) != hipSuccess)
+        return NTT_ERR_HIP;
+      blk -= r[i];
+    }
+    return hipDeviceSynchronize() == hipSuccess ? NTT_OK : NTT_ERR_HIP;
   }
 
   // Column passes 2..p-1 whose table is small enough to stay in L2 (N_i entries of E::TW words <=
@@ -928,7 +939,7 @@ struct PlanImpl final : PlanBase {
 
   unsigned passes_for(unsigned log_x) const override {
     unsigned rr[8] = {0}, p = 0;
-    if (!schedule(log_x, tile_log_of<E>(), E::MIN_COLS_LOG, !E::PASS1_FULL_TABLE && NTT_P_NARROW_FIRST, rr, p))
+    if (!schedule(log_x, tile_log_of<E>(), E::MIN_COLS_LOG, E::NARROW_FIRST, rr, p))
       return 99;
     return p == 0 ? 1 : p;
   }
@@ -989,6 +1000,8 @@ struct PlanImpl final : PlanBase {
         work = d_scratch;
       }
       const uint32_t grid = (uint32_t)((n << il) >> tile_log_of<E>());
+      if (use_full)
+        if (int rc = ensure_full(inverse ? 1 : 0)) return rc;
       // the passes' arguments: column passes 0..npass-2, then the final pass
       PassArgs<E> PA[8];
       unsigned blk = log_n;
@@ -1004,7 +1017,7 @@ struct PlanImpl final : PlanBase {
           const char* v = getenv("NTT_PASS1_FULL");
           return v && atoi(v) > 0;
         }();
-        A.tw_full = (use_full && (i > 0 || E::PASS1_FULL_TABLE || p1_full)) ? d_full + full_off[inverse ? 1 : 0][i] * SCRW
+        A.tw_full = (use_full && (i > 0 || E::PASS1_FULL_TABLE || p1_full)) ? d_fulls[inverse ? 1 : 0] + full_off[i] * SCRW
                                                                              : nullptr;
         if (i > 0 && d_full_sh && full_sh_ok[i]) {
           A.tw_full = d_full_sh + full_sh_off[inverse ? 1 : 0][i] * TW;
@@ -1622,14 +1635,27 @@ namespace {
 struct CachedPlan {
   std::unique_ptr<ntt_plan> plan;
   std::mutex run_mu;
+  uint64_t last_use = 0;
 };
 }  // namespace
 static std::mutex g_cache_mu;
 static std::map<std::tuple<std::vector<uint64_t>, std::vector<uint64_t>, unsigned, unsigned, int>,
-                std::unique_ptr<CachedPlan>>
+                std::shared_ptr<CachedPlan>>
     g_cache;
+static uint64_t g_cache_tick = 0;
+// At most NTT_SHIM_CACHE_PLANS (default 8) cached plans; the least recently used one is dropped
+// when a new key arrives (a call still running on it keeps it alive through its shared_ptr).
+static size_t shim_cache_cap() {
+  static const size_t cap = [] {
+    const char* v = getenv("NTT_SHIM_CACHE_PLANS");
+    const long c = v ? atol(v) : 8;
+    return (size_t)(c > 0 ? c : 1);
+  }();
+  return cap;
+}
 
-static CachedPlan* cached_plan(const uint64_t* p, const uint64_t* g, unsigned limbs64, unsigned log_n, int* rc) {
+static std::shared_ptr<CachedPlan> cached_plan(const uint64_t* p, const uint64_t* g, unsigned limbs64, unsigned log_n,
+                                               int* rc) {
   int dev = 0;
   hipGetDevice(&dev);
   auto key = std::make_tuple(std::vector<uint64_t>(p, p + limbs64), std::vector<uint64_t>(g, g + limbs64), limbs64,
@@ -1637,20 +1663,33 @@ static CachedPlan* cached_plan(const uint64_t* p, const uint64_t* g, unsigned li
   std::lock_guard<std::mutex> lk(g_cache_mu);
   auto it = g_cache.find(key);
   if (it != g_cache.end()) {
+    it->second->last_use = ++g_cache_tick;
     *rc = NTT_OK;
-    return it->second.get();
+    return it->second;
   }
   ntt_plan* pl = nullptr;
   *rc = ntt_plan_create_custom(&pl, p, g, limbs64, log_n, dev);
   if (*rc != NTT_OK) return nullptr;
-  auto& e = g_cache[key];
-  e.reset(new CachedPlan());
+  while (g_cache.size() >= shim_cache_cap()) {
+    auto lru = g_cache.begin();
+    for (auto jt = g_cache.begin(); jt != g_cache.end(); ++jt)
+      if (jt->second->last_use < lru->second->last_use) lru = jt;
+    g_cache.erase(lru);
+  }
+  auto e = std::make_shared<CachedPlan>();
   e->plan.reset(pl);
-  return e.get();
+  e->last_use = ++g_cache_tick;
+  g_cache[key] = e;
+  return e;
+}
+
+extern "C" void ntt_shim_cache_clear(void) {
+  std::lock_guard<std::mutex> lk(g_cache_mu);
+  g_cache.clear();
 }
 
 // forward on the default stream, then wait for the device, under the plan's lock
-static int blocking_forward(CachedPlan* cp, void* d) {
+static int blocking_forward(const std::shared_ptr<CachedPlan>& cp, void* d) {
   std::lock_guard<std::mutex> lk(cp->run_mu);
   int rc = ntt_forward(cp->plan.get(), d, nullptr);
   if (rc == NTT_OK && hipDeviceSynchronize() != hipSuccess) rc = NTT_ERR_HIP;
@@ -1660,7 +1699,7 @@ static int blocking_forward(CachedPlan* cp, void* d) {
 void SSIP(long long* x, long long omega, unsigned log_n) {
   const uint64_t p = 469762049ull, g = (uint64_t)omega;
   int rc = NTT_OK;
-  CachedPlan* pl = cached_plan(&p, &g, 1, log_n, &rc);
+  std::shared_ptr<CachedPlan> pl = cached_plan(&p, &g, 1, log_n, &rc);
   if (!pl) { set_err(rc); return; }
   blocking_forward(pl, x);
 }
@@ -1671,7 +1710,7 @@ int NTT_GZKP_64(long long* data, const void* /*reverse*/, long long len, long lo
   const unsigned log_n = (unsigned)__builtin_ctzll((unsigned long long)len);
   const uint64_t p = 469762049ull, g = (uint64_t)omega;
   int rc = NTT_OK;
-  CachedPlan* pl = cached_plan(&p, &g, 1, log_n, &rc);
+  std::shared_ptr<CachedPlan> pl = cached_plan(&p, &g, 1, log_n, &rc);
   if (!pl) return set_err(rc);
   return blocking_forward(pl, data);
 }
@@ -1686,7 +1725,7 @@ int NTT_GZKP_256(uint32_t* data, uint32_t len, const void* /*reverse*/, uint32_t
     g[i] = (uint64_t)omega[2 * i] | ((uint64_t)omega[2 * i + 1] << 32);
   }
   int rc = NTT_OK;
-  CachedPlan* pl = cached_plan(p, g, 4, log_n, &rc);
+  std::shared_ptr<CachedPlan> pl = cached_plan(p, g, 4, log_n, &rc);
   if (!pl) return set_err(rc);
   return blocking_forward(pl, data);
 }

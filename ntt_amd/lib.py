@@ -65,6 +65,7 @@ PROTOTYPES = {
     "ntt_mplan_destroy": (C.c_int, [_vp]),
     "ntt_count_noncanonical": (C.c_int, [_vp, _vp, C.c_uint64, C.POINTER(C.c_uint64), _vp]),
     "ntt_plan_device_status": (C.c_int, [_vp, C.POINTER(C.c_uint)]),
+    "ntt_shim_cache_clear": (None, []),
     "ntt_inverse_pointwise_batch": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint, _vp]),
     "ntt_twiddle_pack_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint, C.c_uint, C.c_uint, C.c_uint64, C.c_int, C.c_uint64,
                                       _vp]),

@@ -90,6 +90,9 @@ def main() -> None:
             continue
         if not in_k:
             continue
+        if t.startswith(".Lfunc_end"):  # the kernel's end (s_endpgm may also appear on early-exit paths)
+            in_k = False
+            continue
         m = re.match(r"\.loc\s+(\d+)\s+(\d+)", t)
         if m:
             cur = (int(m.group(1)), int(m.group(2)))
@@ -97,9 +100,6 @@ def main() -> None:
         if not t or t.startswith((".", ";")) or t.endswith(":"):
             continue
         op = t.split()[0]
-        if op == "s_endpgm":
-            in_k = False
-            continue
         path = files.get(cur[0], "?") if cur else "?"
         fname = os.path.basename(path)
         if path not in fmaps:
