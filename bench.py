@@ -83,6 +83,9 @@ def parse():
     ap.add_argument("--pieces", type=int, default=None,
                     help="four-step: row pieces whose all-to-all overlaps the next piece's row transforms "
                          "(default: DistNTT.auto_pieces, >= 2^22 elements per piece)")
+    ap.add_argument("--col-pieces", type=int, default=None,
+                    help="four-step: column pieces whose transforms start as their part of the all-to-all "
+                         "arrives (default: as --pieces' default)")
     ap.add_argument("--independent", action="store_true",
                     help="N > 1: one independent transform per rank (weak scaling, no data-path collective)")
     ap.add_argument("--cpu-log-n", type=int, default=22, help="C-oracle single-core sample size (log2)")
@@ -194,7 +197,7 @@ def main():
     if four_step:
         from ntt_amd.distributed import DistNTT
         eng = DistNTT(field_id=args.field, log_n=args.log_n, limbs64=args.limbs, device=local,
-                      host_exchange=rehearsal, pieces=args.pieces)
+                      host_exchange=rehearsal, pieces=args.pieces, col_pieces=args.col_pieces)
         data = eng.empty()
         eng.fill(data, "random", seed=2)
         step = (lambda: eng.inverse(data)) if args.inverse else (lambda: eng.forward(data))
@@ -270,7 +273,7 @@ def main():
                                          f"{world} GPUs, one independent transform per rank (no data-path "
                                          f"collective)")),
                    "transforms_per_step": jobs,
-                   **({"exchange_pieces": len(eng.fs.pieces),
+                   **({"exchange_pieces": len(eng.fs.pieces), "exchange_col_pieces": eng.fs.cp,
                        "split_log_n1_n2": [eng.layout.log_n1, eng.layout.log_n2]} if four_step else {})},
     }
     if four_step:

@@ -247,6 +247,28 @@ int ntt_rplan_forward_rows_range(ntt_rplan* rp, const void* d_x, void* d_send, u
                                  uint64_t row0, uint64_t nrows, void* hip_stream);
 int ntt_rplan_inverse_rows_range(ntt_rplan* rp, const void* d_recv, void* d_out, uint64_t row0, uint64_t nrows,
                                  void* hip_stream);
+/* Pieces on BOTH sides of the exchange (ntt_amd/distributed.py FourStep): row_pieces P_r and
+ * col_pieces P_c, powers of two (<= r and <= c); ra = r / P_r, cm = c / P_c.  Exchange blocks (one
+ * per peer, nvec r c elements each) in these entry points' own layouts:
+ *   forward [i][v][k][ra][cm]: forward_rows_piece(i) writes row piece i of vector `slot`;
+ *     forward_cols_piece(k) transforms column piece k (columns k cm + [0, cm) of the column layout)
+ *     once units (i, v, k) of every peer i have arrived -- row piece i of all vectors is one run
+ *     [i nvec ra c, (i + 1) nvec ra c) of each block, unit (i, v, k) the run of ra cm elements at
+ *     (i nvec + v) ra c + k ra cm;
+ *   inverse [k][i][ra][cm]: inverse_cols_piece(k) (times y, same layout as x, if y != NULL) writes
+ *     column piece k = the run [k r cm, (k + 1) r cm) of each block; inverse_rows_piece(i) transforms
+ *     row piece i once the units (k, i) = runs of ra cm elements at k r cm + i ra cm have arrived.
+ * So the exchange can overlap the row transforms before it and the column transforms after it
+ * (forward), or the column transforms before it and the row transforms after it (inverse).  With
+ * P_r = P_c = 1 the layouts are the [G][nvec][r][c] blocks above. */
+int ntt_rplan_forward_rows_piece(ntt_rplan* rp, const void* d_x, void* d_send, unsigned nvec, unsigned slot,
+                                 unsigned piece, unsigned row_pieces, unsigned col_pieces, void* hip_stream);
+int ntt_rplan_forward_cols_piece(ntt_rplan* rp, const void* d_recv, void* d_x, unsigned nvec, unsigned slot,
+                                 unsigned piece, unsigned row_pieces, unsigned col_pieces, void* hip_stream);
+int ntt_rplan_inverse_cols_piece(ntt_rplan* rp, const void* d_x, const void* d_y, void* d_send, unsigned piece,
+                                 unsigned row_pieces, unsigned col_pieces, void* hip_stream);
+int ntt_rplan_inverse_rows_piece(ntt_rplan* rp, const void* d_recv, void* d_out, unsigned piece, unsigned row_pieces,
+                                 unsigned col_pieces, void* hip_stream);
 /* this rank's row-layout share of the global synthetic vector (kinds as ntt_fill) */
 int ntt_rplan_fill(ntt_rplan* rp, void* d_x, int kind, uint64_t seed, void* hip_stream);
 /* per-launch timing of the row (which = 0) or column (1) transforms, as ntt_plan_last_launch_ms */

@@ -4,15 +4,15 @@
 #include <stdint.h>
 
 #include "ntt.h"
+#include "ntt_kernels.hpp"
 
 namespace ntt {
 
 // Four-step addressing of one local transform (PassArgs::fs and friends, ntt_kernels.hpp).
 struct FsIO {
-  uint32_t fs = 0;                  // FS_MAP_IN | FS_MAP_OUT | FS_IL
+  uint32_t fs = 0;                  // FS_MAP_IN | FS_MAP_OUT | FS_IL | FS_MAP_EPI
   uint32_t il = 0;                  // Mode I: log2 of the interleave
-  uint32_t map_lc = 0;              // chunk-map shift
-  uint64_t map_ps = 0;              // peer stride (elements)
+  FsMap min{}, mout{}, mepi{};      // input, output and epilogue-index maps (PassArgs)
   const void* tw_epi = nullptr;     // final-pass twiddle table (plan_build_fs_table) or null
 };
 

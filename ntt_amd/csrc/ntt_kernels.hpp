@@ -50,6 +50,17 @@ template <class E>
 hipError_t launch_count_noncanonical(const uint32_t* d, size_t n, const ModWords<E::MEMW>& p,
                                      unsigned long long* bad, hipStream_t st);
 
+// Four-step position map (PassArgs::min / mout / mepi): p -> (p >> lc) ps + ((p mod 2^lc) >> lc2) ps2
+// + (b << lc2) + (p mod 2^lc2); lc2 = lc (and ps2 = 0) is the one-level map of round 2.
+struct FsMap {
+  uint32_t lc, lc2;
+  uint64_t ps, ps2;
+  __host__ __device__ size_t operator()(size_t p, size_t b) const {
+    const size_t m = ((size_t)1 << lc) - 1, m2 = ((size_t)1 << lc2) - 1;
+    return (p >> lc) * ps + ((p & m) >> lc2) * ps2 + (b << lc2) + (p & m2);
+  }
+};
+
 template <class E>
 struct PassArgs {
   typename E::Args F;
@@ -73,17 +84,19 @@ struct PassArgs {
   uint32_t src_user;     // column pass: src is the caller's buffer (E::MEMW words/element), not scratch (E::SCRW)
   size_t batch_stride;   // 32-bit words between batched transforms in the caller's buffers (n * E::MEMW)
   // ---- distributed four-step addressing (ntt_rplan_*); fs == 0: plain batched transforms.
-  // Mode B (fs & FS_IL == 0): transform b (= blockIdx.y) of a batch; a mapped position p lives at
-  //   (p >> map_lc) * map_ps + (b << map_lc) + (p mod 2^map_lc): the per-peer chunks [G][batch][2^map_lc]
-  //   of an all-to-all (row transforms: packed output of the forward, chunked input of the inverse).
-  // Mode I (fs & FS_IL): 2^il transforms interleaved, element j of transform b at j 2^il + b (the
-  //   [n1][c] column layout); every pass groups T adjacent transforms, so runs stay contiguous.  A
-  //   mapped input index P lives at (P >> map_lc) * map_ps + (P mod 2^map_lc) (peer chunks of r c).
+  // Mode B (fs & FS_IL == 0): transform b (= blockIdx.y) of a batch, position p (the row transforms:
+  //   packed output of the forward, exchanged input of the inverse).
+  // Mode I (fs & FS_IL): 2^il transforms interleaved, element j of transform b at P = j 2^il + b (the
+  //   [n1][c] column layout and the exchanged blocks); every pass groups T adjacent transforms, so
+  //   runs stay contiguous.  b = 0 in the maps below (P carries it).
+  // A map (FsMap) sends p to (p >> lc) ps + ((p mod 2^lc) >> lc2) ps2 + (b << lc2) + (p mod 2^lc2):
+  //   peer blocks of ps elements, within them column pieces of ps2 elements (lc2 = lc: no pieces).
+  //   min: the first pass's input (FS_MAP_IN, src and src2), mout: the last pass's output
+  //   (FS_MAP_OUT), mepi: the Mode I epilogue-table index (FS_MAP_EPI).
   uint32_t lgp;          // KIND_STOCKHAM: log2 of the number of groups p already combined (bellperson `lgp`)
   uint32_t fs;           // FS_* bits
   uint32_t il;           // Mode I: log2 of the interleave
-  uint32_t map_lc;
-  uint64_t map_ps;
+  FsMap min, mout, mepi;
   const uint32_t* tw_epi;  // final pass: multiply output k of transform b by this table's entry (w R_e,
                            // E::SCRW words; index b N + k in Mode B, k 2^il + b in Mode I) or null
   uint32_t tw_sh;          // column pass: tw_full holds Shoup pairs (canonical w, floor(w B / p); E::TW words
@@ -94,7 +107,7 @@ struct PassArgs {
   const uint32_t* ipn_order; // slab (middle-digit value) of the i-th slab in ticket order (pairs adjacent)
   uint32_t ipn_strips;       // workgroups per slab (R_1 / T)
 };
-enum : uint32_t { FS_MAP_IN = 1u, FS_MAP_OUT = 2u, FS_IL = 4u };
+enum : uint32_t { FS_MAP_IN = 1u, FS_MAP_OUT = 2u, FS_IL = 4u, FS_MAP_EPI = 8u };
 
 // Fused single-launch schedule of a 3-pass transform (k_fused3, BASELINE config 2's "single-kernel"):
 // one persistent launch runs pass 1's, pass 2's and the final pass's tiles, handed between
@@ -185,9 +198,10 @@ hipError_t launch_digitrev_swap(uint32_t* data, const DrevArgs& A, uint32_t batc
 template <class E>
 hipError_t launch_scale_pow(uint32_t* data, uint32_t log_n, uint32_t batch, const uint32_t* lo_s, const uint32_t* hi,
                             uint32_t lo_bits, const typename E::Args& F, hipStream_t st);
-// c = a * b (canonical in/out): mont(mont(a, b), R^2) with r2 in the engine table format
+// c = a * b (canonical in/out): mont(mont(a, b), R^2) with r2 in the engine table format; in_map:
+// element j of a and b is read at (*in_map)(j, 0) (a four-step piece of the column layout)
 template <class E>
 hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, size_t n, const typename E::Args& F,
-                            const uint32_t* d_r2, hipStream_t st);
+                            const uint32_t* d_r2, hipStream_t st, const FsMap* in_map = nullptr);
 
 }  // namespace ntt

@@ -403,23 +403,22 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
   if (!map_in && !single_il) src += bidx * SW;
   if (!map_out && !single_il) dst += bidx * DW;
   const size_t boff = bidx * E::MEMW;  // caller-buffer words (src2)
-  const size_t mlc = ((size_t)1 << A.map_lc) - 1;
   // input element `pos` (transform-relative; Mode I column passes: the interleaved linear index)
   auto in_pos = [&](size_t pos) -> size_t {
     if (single_il) pos = (pos << A.il) + bq;
     if (!map_in) return pos;
-    if (fs_il) return (pos >> A.map_lc) * A.map_ps + (pos & mlc);
-    return (pos >> A.map_lc) * A.map_ps + ((size_t)bq << A.map_lc) + (pos & mlc);
+    return A.min(pos, fs_il ? 0 : bq);
   };
   // output element (pre-map position as above) -> address; epilogue-table index of the same element
   auto out_pos = [&](size_t pos) -> size_t {
     if (single_il) pos = (pos << A.il) + bq;
     if (!map_out) return pos;
-    return (pos >> A.map_lc) * A.map_ps + ((size_t)bq << A.map_lc) + (pos & mlc);
+    return A.mout(pos, fs_il ? 0 : bq);
   };
   auto epi_idx = [&](size_t pos) -> size_t {
-    if (single_il) return (pos << A.il) + bq;
-    return fs_il ? pos : (((size_t)bq << A.log_n) + pos);
+    if (!fs_il) return ((size_t)bq << A.log_n) + pos;
+    if (single_il) pos = (pos << A.il) + bq;
+    return (A.fs & FS_MAP_EPI) ? A.mepi(pos, 0) : pos;
   };
 
   // ------------------------------------------------------------------ workgroup geometry
@@ -517,7 +516,7 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
         }
         if constexpr (PRO == PRO_PW) {
           uint32_t y[E::W];
-          E::load(y, A.src2 + boff, pos);
+          E::load(y, A.src2 + boff, in_pos(pos));  // src2 has src's layout (a four-step piece: mapped)
           E::mulv(x[j * Q + d], y, A.F);  // canonical inputs: < 3p, normalised
         } else if constexpr (PRO == PRO_COSET) {
           typename E::Tw u;
@@ -1417,12 +1416,14 @@ __global__ void k_fill_iota(uint32_t* __restrict__ dst, size_t n, FillMap fm) {
 
 template <class E>
 __global__ void k_pointwise_mul(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, uint32_t* __restrict__ c,
-                                size_t n, const typename E::Args F, const uint32_t* __restrict__ r2) {
+                                size_t n, const typename E::Args F, const uint32_t* __restrict__ r2, const FsMap m,
+                                const uint32_t mapped) {
   NTT_GRID_STRIDE(j, n) {
     uint32_t x[E::W], y[E::W];
     typename E::Tw z;  // R_e mod p as a twiddle: mulv leaves x y / R_e
-    E::load(x, a, j);
-    E::load(y, b, j);
+    const size_t src = mapped ? m(j, 0) : j;  // a four-step piece gathered from the column layout
+    E::load(x, a, src);
+    E::load(y, b, src);
     E::tload(z, r2, 0);
     E::mulv(x, y, F);
     E::mul(x, z, F);
@@ -1596,9 +1597,10 @@ hipError_t launch_fill(int kind, uint32_t* dst, size_t n, uint64_t seed, uint32_
 
 template <class E>
 hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, size_t n, const typename E::Args& F,
-                            const uint32_t* d_r2, hipStream_t st) {
+                            const uint32_t* d_r2, hipStream_t st, const FsMap* in_map) {
   const uint32_t blocks = grid_1d(n);
-  hipLaunchKernelGGL((k_pointwise_mul<E>), dim3(blocks), dim3(256), 0, st, a, b, c, n, F, d_r2);
+  const FsMap m = in_map ? *in_map : FsMap{};
+  hipLaunchKernelGGL((k_pointwise_mul<E>), dim3(blocks), dim3(256), 0, st, a, b, c, n, F, d_r2, m, in_map ? 1u : 0u);
   return hipGetLastError();
 }
 
@@ -1635,7 +1637,7 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
   template hipError_t launch_digitrev_swap<E>(uint32_t*, const DrevArgs&, uint32_t, hipStream_t);                  \
   template hipError_t launch_final_ipn<E>(int, uint32_t*, const PassArgs<E>&, uint32_t, hipStream_t);              \
   template hipError_t launch_pointwise<E>(const uint32_t*, const uint32_t*, uint32_t*, size_t,                     \
-                                          const typename E::Args&, const uint32_t*, hipStream_t);                  \
+                                          const typename E::Args&, const uint32_t*, hipStream_t, const FsMap*);    \
   template hipError_t launch_build_tw<E>(uint32_t*, size_t, uint32_t, uint32_t, uint32_t, const uint32_t*,        \
                                          const uint32_t*, uint32_t, const typename E::Args&, hipStream_t,          \
                                          const uint32_t*, const uint32_t*);                                        \

@@ -413,6 +413,7 @@ struct PlanImpl final : PlanBase {
     if (d_coset_full) hipFree(d_coset_full);
     if (d_sync) hipFree(d_sync);
     if (d_ipn) hipFree(d_ipn);
+    if (d_pw) hipFree(d_pw);
     for (auto& row : ev)
       for (auto& e : row)
         if (e) hipEventDestroy(e);
@@ -962,10 +963,11 @@ struct PlanImpl final : PlanBase {
     const uint32_t il = (io && (io->fs & FS_IL)) ? io->il : 0u;
     auto set_fs = [&](PassArgs<E>& A, uint32_t bits) {
       if (!io) return;
-      A.fs = io->fs & (bits | FS_IL);
+      A.fs = io->fs & (bits | FS_IL | FS_MAP_EPI);
       A.il = il;
-      A.map_lc = io->map_lc;
-      A.map_ps = io->map_ps;
+      A.min = io->min;
+      A.mout = io->mout;
+      A.mepi = io->mepi;
     };
     if (io && (log_n == 0 || npass == 0)) return NTT_ERR_ARG;  // four-step pieces are >= 8 points
     if (log_n == 0) {
@@ -1243,15 +1245,35 @@ struct PlanImpl final : PlanBase {
     auto pin = static_cast<const uint32_t*>(in);
     auto pout = static_cast<uint32_t*>(out);
     if (!in2) return run_io(pin, nullptr, pout, batch, inverse, st, nullptr, nullptr, &io);
-    if (!inverse || (io.fs & FS_MAP_IN)) return NTT_ERR_ARG;  // the product is taken at the inverse's load
+    if (!inverse) return NTT_ERR_ARG;  // the product is taken at the inverse's load
     const size_t count = (size_t)n * ((io.fs & FS_IL) ? (1ull << io.il) : batch);
-    if (polymul_fusable() && npass >= 2) {
+    if (polymul_fusable() && npass >= 2) {  // in2 read through the input map like in
       if (int rc = ensure_polymul_table()) return rc;
       return run_io(pin, static_cast<const uint32_t*>(in2), pout, batch, true, st, nullptr, nullptr, &io);
     }
-    if (int rc = pointwise_n(pin, static_cast<const uint32_t*>(in2), pout, count, st)) return rc;
-    return run_io(pout, nullptr, pout, batch, true, st, nullptr, nullptr, &io);
+    if (!(io.fs & (FS_MAP_IN | FS_MAP_OUT))) {  // same layout in and out: the product in place in out
+      if (int rc = pointwise_n(pin, static_cast<const uint32_t*>(in2), pout, count, st)) return rc;
+      return run_io(pout, nullptr, pout, batch, true, st, nullptr, nullptr, &io);
+    }
+    // a mapped piece (the column pieces of ntt_rplan_inverse_cols_piece): the product gathered into a
+    // plan-owned buffer first (out's other pieces may still be in flight)
+    if (count > pw_elems) {
+      if (d_pw) hipFree(d_pw);
+      d_pw = nullptr;
+      pw_elems = 0;
+      if (hipMalloc(&d_pw, count * MEMW * 4) != hipSuccess) return NTT_ERR_HIP;
+      pw_elems = count;
+    }
+    const size_t off = (flags & NTT_PLAN_MONTGOMERY_IO) ? off_rm : off_r2;
+    if (launch_pointwise<E>(pin, static_cast<const uint32_t*>(in2), d_pw, count, Ff, d_tab + off, st,
+                            (io.fs & FS_MAP_IN) ? &io.min : nullptr) != hipSuccess)
+      return NTT_ERR_HIP;
+    FsIO io2 = io;
+    io2.fs &= ~FS_MAP_IN;
+    return run_io(d_pw, nullptr, pout, batch, true, st, nullptr, nullptr, &io2);
   }
+  uint32_t* d_pw = nullptr;  // gathered pointwise products of mapped pieces (run_fs), on first use
+  size_t pw_elems = 0;
 
   int build_fs_table(void* table, unsigned log_rows, unsigned log_cols, uint64_t row0, uint64_t col0, bool inverse,
                      hipStream_t st) override {

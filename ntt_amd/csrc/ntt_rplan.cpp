@@ -68,6 +68,11 @@ hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
 
 bool nvec_ok(unsigned nvec, unsigned slot) { return (nvec == 1 || nvec == 2) && slot < nvec; }
 
+// one-level map: p -> (p >> lc) ps + (b << lc) + (p mod 2^lc)
+FsMap map1(unsigned lc, uint64_t ps) { return FsMap{lc, lc, ps, 0}; }
+// two-level map: peer blocks of ps, column pieces of ps2 within them (FsMap, ntt_kernels.hpp)
+FsMap map2(unsigned lc, uint64_t ps, unsigned lc2, uint64_t ps2) { return FsMap{lc, lc2, ps, ps2}; }
+
 // The split n = n1 n2 (log_n2 returned): fewest pass kernels over the row (length n2) and column
 // (length n1) transforms, the most balanced split among equals.  2^24 on the 256-bit engines: 12 + 12
 // takes 2 + 2 passes, 14 + 10 takes 2 + 1 (the rows one workgroup tile each) -- as many HBM passes
@@ -96,6 +101,23 @@ constexpr uint64_t kMaxRowsPerLaunch = 1ull << 15;
 bool range_ok(const ntt_rplan* rp, uint64_t row0, uint64_t nrows) {
   const uint64_t r = 1ull << rp->log_r;
   return nrows >= 1 && row0 < r && nrows <= r - row0;
+}
+
+// Pieces of the two-sided pipelined exchange (FourStep, ntt_amd/distributed.py): P_r row pieces of
+// ra = r / P_r rows, P_c column pieces of cm = c / P_c columns (powers of two).  Exchange blocks, one
+// per peer of nvec r c elements:
+//   forward [i][v][k][ra][cm]  written by forward_rows_piece (row piece i), read by forward_cols_piece
+//                              (column piece k: rows j1 = h r + i ra + a' of every peer h)
+//   inverse [k][i][ra][cm]     written by inverse_cols_piece (column piece k), read by
+//                              inverse_rows_piece (row piece i)
+// With P_r = P_c = 1 both are the [G][nvec][r][c] blocks of the row-range entry points.
+bool pieces_ok(const ntt_rplan* rp, unsigned rpc, unsigned cpc, unsigned& lra, unsigned& lcm) {
+  if (rpc == 0 || cpc == 0 || (rpc & (rpc - 1)) || (cpc & (cpc - 1))) return false;
+  const unsigned lp = (unsigned)__builtin_ctz(rpc), lq = (unsigned)__builtin_ctz(cpc);
+  if (lp > rp->log_r || lq > rp->log_c) return false;
+  lra = rp->log_r - lp;
+  lcm = rp->log_c - lq;
+  return true;
 }
 
 }  // namespace
@@ -179,8 +201,7 @@ int ntt_rplan_forward_rows_range(ntt_rplan* rp, const void* d_x, void* d_send, u
   // and the Mode B output map (row a lands at a c within every peer chunk) by row0
   FsIO io;
   io.fs = FS_MAP_OUT;
-  io.map_lc = rp->log_c;
-  io.map_ps = nvec * rp->chunk();
+  io.mout = map1(rp->log_c, nvec * rp->chunk());
   io.tw_epi = static_cast<const char*>(rp->tab_fwd) + (row0 << rp->log_n2) * plan_table_entry_bytes(rp->tw);
   const void* src = static_cast<const char*>(d_x) + (row0 << rp->log_n2) * rp->elem_bytes;
   void* dst = static_cast<char*>(d_send) + (slot * rp->chunk() + (row0 << rp->log_c)) * rp->elem_bytes;
@@ -198,8 +219,7 @@ int ntt_rplan_forward_cols(ntt_rplan* rp, const void* d_recv, void* d_x, unsigne
   FsIO io;
   io.fs = FS_IL | (nvec > 1 ? FS_MAP_IN : 0u);
   io.il = rp->log_c;
-  io.map_lc = rp->log_r + rp->log_c;
-  io.map_ps = nvec * rp->chunk();
+  io.min = map1(rp->log_r + rp->log_c, nvec * rp->chunk());
   const void* src = static_cast<const char*>(d_recv) + slot * rp->chunk() * rp->elem_bytes;
   return plan_run_fs(rp->cols, src, nullptr, d_x, 1, false, io, S(s));
 }
@@ -227,8 +247,7 @@ int ntt_rplan_inverse_rows_range(ntt_rplan* rp, const void* d_recv, void* d_out,
   DeviceScope scope(rp->device);
   FsIO io;
   io.fs = FS_MAP_IN;
-  io.map_lc = rp->log_c;
-  io.map_ps = rp->chunk();
+  io.min = map1(rp->log_c, rp->chunk());
   const void* src = static_cast<const char*>(d_recv) + (row0 << rp->log_c) * rp->elem_bytes;
   void* dst = static_cast<char*>(d_out) + (row0 << rp->log_n2) * rp->elem_bytes;
   return plan_run_fs(rp->rows, src, nullptr, dst, (unsigned)nrows, true, io, S(s));
@@ -237,6 +256,90 @@ int ntt_rplan_inverse_rows_range(ntt_rplan* rp, const void* d_recv, void* d_out,
 int ntt_rplan_inverse_rows(ntt_rplan* rp, const void* d_recv, void* d_out, void* s) {
   if (!rp) return NTT_ERR_ARG;
   return ntt_rplan_inverse_rows_range(rp, d_recv, d_out, 0, 1ull << rp->log_r, s);
+}
+
+int ntt_rplan_forward_rows_piece(ntt_rplan* rp, const void* d_x, void* d_send, unsigned nvec, unsigned slot,
+                                 unsigned piece, unsigned row_pieces, unsigned col_pieces, void* s) {
+  unsigned lra = 0, lcm = 0;
+  if (!rp || !d_x || !d_send || !nvec_ok(nvec, slot) || !pieces_ok(rp, row_pieces, col_pieces, lra, lcm) ||
+      piece >= row_pieces)
+    return NTT_ERR_ARG;
+  DeviceScope scope(rp->device);
+  const uint64_t ra = 1ull << lra, cm = 1ull << lcm, c = 1ull << rp->log_c;
+  for (uint64_t a0 = 0; a0 < ra; a0 += kMaxRowsPerLaunch) {
+    const uint64_t m = ra - a0 < kMaxRowsPerLaunch ? ra - a0 : kMaxRowsPerLaunch;
+    const uint64_t row0 = piece * ra + a0;
+    // output k2 of launch row b: peer k2 >> log c, column piece (k2 mod c) >> log cm, row a0 + b
+    FsIO io;
+    io.fs = FS_MAP_OUT;
+    io.mout = map2(rp->log_c, nvec * rp->chunk(), lcm, ra * cm);
+    io.tw_epi = static_cast<const char*>(rp->tab_fwd) + (row0 << rp->log_n2) * plan_table_entry_bytes(rp->tw);
+    const void* src = static_cast<const char*>(d_x) + (row0 << rp->log_n2) * rp->elem_bytes;
+    void* dst = static_cast<char*>(d_send) + ((piece * nvec + slot) * ra * c + a0 * cm) * rp->elem_bytes;
+    if (int rc = plan_run_fs(rp->rows, src, nullptr, dst, (unsigned)m, false, io, S(s))) return rc;
+  }
+  return NTT_OK;
+}
+
+int ntt_rplan_forward_cols_piece(ntt_rplan* rp, const void* d_recv, void* d_x, unsigned nvec, unsigned slot,
+                                 unsigned piece, unsigned row_pieces, unsigned col_pieces, void* s) {
+  unsigned lra = 0, lcm = 0;
+  if (!rp || !d_recv || !d_x || !nvec_ok(nvec, slot) || !pieces_ok(rp, row_pieces, col_pieces, lra, lcm) ||
+      piece >= col_pieces)
+    return NTT_ERR_ARG;
+  DeviceScope scope(rp->device);
+  const uint64_t ra = 1ull << lra, cm = 1ull << lcm, c = 1ull << rp->log_c;
+  // cm interleaved transforms; element j1 = (h P_r + i) ra + a' of transform kc' at that block's unit
+  FsIO io;
+  io.fs = FS_IL | FS_MAP_IN | FS_MAP_OUT;
+  io.il = lcm;
+  io.min = map1(lra + lcm, nvec * ra * c);
+  io.mout = map1(lcm, c);  // column layout [n1][c], columns piece cm + [0, cm)
+  const void* src = static_cast<const char*>(d_recv) + (slot * ra * c + piece * ra * cm) * rp->elem_bytes;
+  void* dst = static_cast<char*>(d_x) + piece * cm * rp->elem_bytes;
+  return plan_run_fs(rp->cols, src, nullptr, dst, 1, false, io, S(s));
+}
+
+int ntt_rplan_inverse_cols_piece(ntt_rplan* rp, const void* d_x, const void* d_y, void* d_send, unsigned piece,
+                                 unsigned row_pieces, unsigned col_pieces, void* s) {
+  unsigned lra = 0, lcm = 0;
+  if (!rp || !d_x || !d_send || !pieces_ok(rp, row_pieces, col_pieces, lra, lcm) || piece >= col_pieces)
+    return NTT_ERR_ARG;
+  DeviceScope scope(rp->device);
+  const uint64_t cm = 1ull << lcm, c = 1ull << rp->log_c;
+  FsIO io;
+  io.fs = FS_IL | FS_MAP_IN | FS_MAP_OUT | FS_MAP_EPI;
+  io.il = lcm;
+  io.min = map1(lcm, c);                          // columns piece cm + [0, cm) of [n1][c] (and of y)
+  io.mout = map1(rp->log_r + lcm, rp->chunk());  // j1 = h r + a -> block h, unit piece, row a
+  io.mepi = map1(lcm, c);                         // the [n1][c] epilogue table
+  io.tw_epi = static_cast<const char*>(rp->tab_inv) + piece * cm * plan_table_entry_bytes(rp->tw);
+  const size_t off = piece * cm * rp->elem_bytes;
+  const void* src = static_cast<const char*>(d_x) + off;
+  const void* y = d_y ? static_cast<const char*>(d_y) + off : nullptr;
+  void* dst = static_cast<char*>(d_send) + (piece << (rp->log_r + lcm)) * rp->elem_bytes;
+  return plan_run_fs(rp->cols, src, y, dst, 1, true, io, S(s));
+}
+
+int ntt_rplan_inverse_rows_piece(ntt_rplan* rp, const void* d_recv, void* d_out, unsigned piece, unsigned row_pieces,
+                                 unsigned col_pieces, void* s) {
+  unsigned lra = 0, lcm = 0;
+  if (!rp || !d_recv || !d_out || !pieces_ok(rp, row_pieces, col_pieces, lra, lcm) || piece >= row_pieces)
+    return NTT_ERR_ARG;
+  DeviceScope scope(rp->device);
+  const uint64_t ra = 1ull << lra, cm = 1ull << lcm;
+  for (uint64_t a0 = 0; a0 < ra; a0 += kMaxRowsPerLaunch) {
+    const uint64_t m = ra - a0 < kMaxRowsPerLaunch ? ra - a0 : kMaxRowsPerLaunch;
+    const uint64_t row0 = piece * ra + a0;
+    // input k2 of launch row b: block k2 >> log c, unit (k2 mod c) >> log cm, row row0 + b
+    FsIO io;
+    io.fs = FS_MAP_IN;
+    io.min = map2(rp->log_c, rp->chunk(), lcm, (1ull << rp->log_r) * cm);
+    const void* src = static_cast<const char*>(d_recv) + row0 * cm * rp->elem_bytes;
+    void* dst = static_cast<char*>(d_out) + (row0 << rp->log_n2) * rp->elem_bytes;
+    if (int rc = plan_run_fs(rp->rows, src, nullptr, dst, (unsigned)m, true, io, S(s))) return rc;
+  }
+  return NTT_OK;
 }
 
 int ntt_rplan_fill(ntt_rplan* rp, void* d_x, int kind, uint64_t seed, void* s) {

@@ -73,38 +73,64 @@ class Layout:
         return self.rank * self.c + kc + self.n2 * k1
 
 
+def pow2_pieces(k, limit: int) -> int:
+    """The piece count actually used: the largest power of two <= min(k, limit) (pieces are uniform,
+    so that every exchange unit is one contiguous run of the buffer layouts below)."""
+    k = max(1, min(int(k), int(limit)))
+    return 1 << (k.bit_length() - 1)
+
+
 class FourStep:
     """Per-rank four-step schedule over an engine (local compute) and an exchange (all-to-all).
 
-    Engine interface (one rank): ``forward_rows(x, send, nvec, slot, row0, nrows)`` (rows [row0,
-    row0 + nrows) of the row layout -> their runs of every peer chunk), ``forward_cols(recv, x, nvec,
-    slot)`` (received chunks -> column layout), ``inverse_cols(x, y, send)`` (column layout, times y
-    if given -> peer chunks), ``inverse_rows(recv, out, row0, nrows)`` (-> rows of the row layout),
-    ``empty(count)``.  Buffers hold [G][nvec][r][c] elements (a peer chunk is [r][c]).
+    The local steps run in pieces so that the all-to-all overlaps compute on BOTH sides of it:
+    P_r row pieces (r / P_r rows each) and P_c column pieces (c / P_c columns each, both powers of two).
 
-    Exchange interface: ``start(send, recv, nvec, row0, nrows)`` moves rows [row0, row0 + nrows) of
-    every peer chunk (all nvec vectors) and returns a handle, ordered after the compute enqueued so
-    far; ``wait(handle)`` orders later compute after it.  A plain callable ``exchange(send, recv)``
-    (one all-to-all of whole chunks) is accepted too and runs the schedule unpipelined.
+    * forward: the row transforms of row piece i are exchanged while those of piece i + 1 run; the
+      last row piece goes out column piece by column piece, and the column transforms of piece k start
+      as soon as its part has arrived (the earlier row pieces are in by then);
+    * inverse: mirrored -- the column transforms of column piece k are exchanged while piece k + 1
+      transforms; the last column piece goes out row piece by row piece, and the inverse row
+      transforms of piece i start as soon as its part has arrived.
 
-    With ``pieces`` > 1 the row steps run in pieces of r / pieces rows: the forward exchanges each
-    piece while the row transforms of the next one run, the inverse transforms each piece as soon as
-    it has arrived -- the all-to-all overlaps the local transforms instead of following them.
+    A column piece is c / P_c whole length-n1 transforms and a row piece r / P_r whole length-n2
+    transforms, so no transform ever waits for more than its own inputs.  Exchange buffers hold one
+    block of nvec * r * c elements per peer (ntt.h, ntt_rplan_*_piece):
+
+    * forward blocks [i][v][k][r / P_r][c / P_c]: row piece i of every vector is one contiguous run,
+      and so is each (i, v, k) unit;
+    * inverse blocks [k][i][r / P_r][c / P_c] (nvec = 1): column piece k is one run, and so is each
+      (k, i) unit.
+
+    With P_r = P_c = 1 both are [G][nvec][r][c].
+
+    Engine interface (one rank): ``forward_rows_piece(x, send, nvec, slot, i, P_r, P_c)``,
+    ``forward_cols_piece(recv, x, nvec, slot, k, P_r, P_c)``, ``inverse_cols_piece(x, y, send, k,
+    P_r, P_c)`` (column layout, times y if given), ``inverse_rows_piece(recv, out, i, P_r, P_c)``,
+    ``empty(count)``.  Exchange interface: ``start(send, recv, peer_stride, runs)`` moves the runs
+    [(offset, length), ...] (elements, relative to each peer's block of ``peer_stride`` elements) from
+    every rank to every rank, ordered after the compute enqueued so far, and returns a handle;
+    ``wait(handle)`` orders later compute after it.  A plain callable ``exchange(send, recv)`` (one
+    all-to-all of whole blocks) is accepted too and runs the schedule unpipelined.
     """
 
-    def __init__(self, layout: Layout, engine, exchange=None, pieces: int = 1):
+    def __init__(self, layout: Layout, engine, exchange=None, pieces: int = 1, col_pieces: int = 1):
         self.L = layout
         self.eng = engine
         if exchange is not None and not hasattr(exchange, "start"):
-            exchange, pieces = _WholeExchange(exchange), 1
+            exchange, pieces, col_pieces = _WholeExchange(exchange), 1, 1
         self.exchange = exchange
-        self.pieces = self.piece_ranges(layout.r, pieces)
+        self.rp = pow2_pieces(pieces, layout.r)
+        self.cp = pow2_pieces(col_pieces, layout.c)
+        ra = layout.r // self.rp
+        self.pieces = [(i * ra, ra) for i in range(self.rp)]  # row pieces (first row, rows)
         self.send = engine.empty(layout.local_n)
         self.recv = engine.empty(layout.local_n)
-        self.send2 = self.recv2 = None  # [G][2][chunk]: the polymul's batched exchange, on first use
+        self.send2 = self.recv2 = None  # the polymul's two-vector exchange buffers, on first use
 
     @staticmethod
     def piece_ranges(r: int, pieces: int):
+        """Near-equal row ranges (the row-range entry points ntt_rplan_*_rows_range, ntt_mplan)."""
         k = max(1, min(int(pieces), r))
         step = -(-r // k)
         return [(a, min(step, r - a)) for a in range(0, r, step)]
@@ -115,36 +141,64 @@ class FourStep:
             self.recv2 = self.eng.empty(2 * self.L.local_n)
         return self.send2, self.recv2
 
-    # ---- forward: row layout -> column layout (in place on x)
-    def forward_rows_piece(self, x, i, nvec=1, slot=0, send=None):
-        a0, ra = self.pieces[i]
-        self.eng.forward_rows(x, self.send if send is None else send, nvec, slot, a0, ra)
+    # ---- exchange units (element runs within one peer block)
+    def fwd_runs(self, nvec, i, k=None):
+        L = self.L
+        ra, cm = L.r // self.rp, L.c // self.cp
+        base = i * nvec * ra * L.c
+        if k is None:
+            return [(base, nvec * ra * L.c)]
+        return [(base + v * ra * L.c + k * ra * cm, ra * cm) for v in range(nvec)]
+
+    def inv_runs(self, k, i=None):
+        L = self.L
+        ra, cm = L.r // self.rp, L.c // self.cp
+        base = k * L.r * cm
+        return [(base, L.r * cm)] if i is None else [(base + i * ra * cm, ra * cm)]
+
+    # ---- forward: row layout -> column layout (in place on each x)
+    def _forward(self, xs, send, recv):
+        nvec, ps = len(xs), len(xs) * self.L.chunk
+        early, tail = [], []
+        for i in range(self.rp):
+            for v, x in enumerate(xs):
+                self.eng.forward_rows_piece(x, send, nvec, v, i, self.rp, self.cp)
+            if i < self.rp - 1 or self.cp == 1:
+                early.append(self.exchange.start(send, recv, ps, self.fwd_runs(nvec, i)))
+            else:
+                tail = [self.exchange.start(send, recv, ps, self.fwd_runs(nvec, i, k)) for k in range(self.cp)]
+        for h in early:
+            self.exchange.wait(h)
+        for k in range(self.cp):
+            if tail:
+                self.exchange.wait(tail[k])
+            for v, x in enumerate(xs):
+                self.eng.forward_cols_piece(recv, x, nvec, v, k, self.rp, self.cp)
 
     def forward(self, x):
-        hs = []
-        for i, (a0, ra) in enumerate(self.pieces):
-            self.forward_rows_piece(x, i)
-            hs.append(self.exchange.start(self.send, self.recv, 1, a0, ra))
-        for h in hs:
-            self.exchange.wait(h)
-        self.eng.forward_cols(self.recv, x, 1, 0)
+        self._forward([x], self.send, self.recv)
         return x
 
-    # ---- inverse: column layout -> row layout (in place on x, or into out with a pointwise factor y)
-    def inverse_rows_piece(self, out, i):
-        a0, ra = self.pieces[i]
-        self.eng.inverse_rows(self.recv, out, a0, ra)
-
-    def _inverse_tail(self, out):
-        hs = [self.exchange.start(self.send, self.recv, 1, a0, ra) for a0, ra in self.pieces]
-        for i, h in enumerate(hs):
+    # ---- inverse: column layout (times y) -> row layout in out
+    def _inverse(self, x, y, out):
+        ps = self.L.chunk
+        early, tail = [], []
+        for k in range(self.cp):
+            self.eng.inverse_cols_piece(x, y, self.send, k, self.rp, self.cp)
+            if k < self.cp - 1 or self.rp == 1:
+                early.append(self.exchange.start(self.send, self.recv, ps, self.inv_runs(k)))
+            else:
+                tail = [self.exchange.start(self.send, self.recv, ps, self.inv_runs(k, i)) for i in range(self.rp)]
+        for h in early:
             self.exchange.wait(h)
-            self.inverse_rows_piece(out, i)
+        for i in range(self.rp):
+            if tail:
+                self.exchange.wait(tail[i])
+            self.eng.inverse_rows_piece(self.recv, out, i, self.rp, self.cp)
         return out
 
     def inverse(self, x):
-        self.eng.inverse_cols(x, None, self.send)
-        return self._inverse_tail(x)
+        return self._inverse(x, None, x)
 
     # ---- polynomial multiply: row-layout a, b -> row-layout out = a * b (cyclic, length n).
     # a and b are left holding their column-layout forward transforms (unless out aliases them).
@@ -153,37 +207,26 @@ class FourStep:
             self.forward(a)
         else:
             send2, recv2 = self.pair_buffers()
-            hs = []
-            for i, (a0, ra) in enumerate(self.pieces):
-                self.forward_rows_piece(a, i, 2, 0, send2)
-                self.forward_rows_piece(b, i, 2, 1, send2)
-                hs.append(self.exchange.start(send2, recv2, 2, a0, ra))
-            for h in hs:
-                self.exchange.wait(h)
-            self.eng.forward_cols(recv2, a, 2, 0)
-            self.eng.forward_cols(recv2, b, 2, 1)
-        self.eng.inverse_cols(a, b, self.send)
-        return self._inverse_tail(out)
+            self._forward([a, b], send2, recv2)  # a and b in every exchange unit
+        return self._inverse(a, b, out)
 
 
 class _WholeExchange:
-    """Adapter for a plain ``exchange(send, recv)`` callable: whole-chunk all-to-all, one piece."""
+    """Adapter for a plain ``exchange(send, recv)`` callable: whole-block all-to-all, one piece."""
 
     def __init__(self, fn):
         self.fn = fn
 
-    def start(self, send, recv, nvec, row0, nrows):
+    def start(self, send, recv, peer_stride, runs):
         self.fn(send, recv)
 
     def wait(self, handle):
         pass
 
 
-def piece_views(buf, world: int, nvec: int, r: int, c: int, row0: int, nrows: int):
-    """[peer][vec] views of rows [row0, row0 + nrows) of a [G][nvec][r][c] exchange buffer: each a
-    contiguous run of nrows * c elements."""
-    b = buf.view(world, nvec, r * c, *buf.shape[1:])
-    return [[b[g, v, row0 * c:(row0 + nrows) * c] for v in range(nvec)] for g in range(world)]
+def run_views(buf, world: int, peer_stride: int, runs):
+    """[peer][run] views of an exchange buffer: run (off, len) of every peer block."""
+    return [[buf[g * peer_stride + off:g * peer_stride + off + ln] for off, ln in runs] for g in range(world)]
 
 
 class RankPlan:
@@ -221,6 +264,7 @@ class RankPlan:
         return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 
     def forward_rows(self, x, send, nvec, slot, row0=0, nrows=None):
+        """Rows [row0, row0 + nrows) -> [G][nvec][r][c] blocks (the row-range entry point, ntt_mplan's layout)."""
         nrows = self.layout.r - row0 if nrows is None else nrows
         self._L.check(self.lib.ntt_rplan_forward_rows_range(self.handle, self._p(x), self._p(send), nvec, slot, row0,
                                                             nrows, self._s(x)), "ntt_rplan_forward_rows_range")
@@ -237,6 +281,23 @@ class RankPlan:
         nrows = self.layout.r - row0 if nrows is None else nrows
         self._L.check(self.lib.ntt_rplan_inverse_rows_range(self.handle, self._p(recv), self._p(out), row0, nrows,
                                                             self._s(out)), "ntt_rplan_inverse_rows_range")
+
+    # ---- the piece entry points FourStep schedules (ntt_rplan_*_piece)
+    def forward_rows_piece(self, x, send, nvec, slot, i, rp, cp):
+        self._L.check(self.lib.ntt_rplan_forward_rows_piece(self.handle, self._p(x), self._p(send), nvec, slot, i, rp,
+                                                            cp, self._s(x)), "ntt_rplan_forward_rows_piece")
+
+    def forward_cols_piece(self, recv, x, nvec, slot, k, rp, cp):
+        self._L.check(self.lib.ntt_rplan_forward_cols_piece(self.handle, self._p(recv), self._p(x), nvec, slot, k, rp,
+                                                            cp, self._s(x)), "ntt_rplan_forward_cols_piece")
+
+    def inverse_cols_piece(self, x, y, send, k, rp, cp):
+        self._L.check(self.lib.ntt_rplan_inverse_cols_piece(self.handle, self._p(x), self._p(y), self._p(send), k, rp,
+                                                            cp, self._s(x)), "ntt_rplan_inverse_cols_piece")
+
+    def inverse_rows_piece(self, recv, out, i, rp, cp):
+        self._L.check(self.lib.ntt_rplan_inverse_rows_piece(self.handle, self._p(recv), self._p(out), i, rp, cp,
+                                                            self._s(out)), "ntt_rplan_inverse_rows_piece")
 
     def fill(self, t, kind: str = "random", seed: int = 1):
         k = {"iota": 0, "random": 1}[kind]
@@ -259,30 +320,37 @@ class DistNTT:
 
     The default process group must be initialised (``nccl`` backend = RCCL on ROCm).  ``forward``
     takes this rank's row-layout share and leaves its column-layout share in place; ``inverse`` the
-    reverse.  See module docstring for the layouts.  The all-to-all runs in ``pieces`` row pieces,
-    each an asynchronous RCCL all-to-all on the communicator's stream, overlapping the row transforms
-    (FourStep).
+    reverse.  See module docstring for the layouts.  The all-to-all runs in units of ``pieces`` row
+    pieces x ``col_pieces`` column pieces, each an asynchronous RCCL all-to-all on the communicator's
+    stream, overlapping the local transforms on both sides of the exchange (FourStep).
     """
 
     # A piece's row transforms must still fill the GPU: every pass of a local transform launches one
     # 1024-element workgroup tile per 1024 elements, and 256 CUs x 4 resident workgroups want several
     # rounds of them.  Measured on one GPU (profiles/r02_pipe/, configs.jsonl): 2^28 over 8 virtual
     # ranks (2^25 per rank) 34.5 -> 33.5 ms with 4 pieces; 2^24 polymul over 8 (2^21 per rank)
-    # 6.8 -> 8.0 ms with 4 pieces (half-empty launches).
+    # 6.8 -> 8.0 ms with 4 pieces (half-empty launches).  Column pieces only have to cover the last
+    # row piece's exchange, so they may be smaller: 2^24 over 2 virtual ranks with 4 x 4 pieces (2^21
+    # elements per column piece) cost 1.5 % over 1 x 1, 2^24 over 8 with 2 x 2 (2^20) 11 %
+    # (profiles/r03_pieces/).
     MIN_PIECE_ELEMS = 1 << 22
+    MIN_COL_PIECE_ELEMS = 1 << 21
 
     @classmethod
-    def auto_pieces(cls, local_n: int, cap: int = 8) -> int:
+    def auto_pieces(cls, local_n: int, cap: int = 8, min_elems: Optional[int] = None) -> int:
+        m = cls.MIN_PIECE_ELEMS if min_elems is None else min_elems
         k = 1
-        while k < cap and local_n // (2 * k) >= cls.MIN_PIECE_ELEMS:
+        while k < cap and local_n // (2 * k) >= m:
             k *= 2
         return k
 
     def __init__(self, field_id: int = 1, log_n: int = 24, limbs64: int = 4, device: Optional[int] = None,
-                 group=None, host_exchange: bool = False, pieces: Optional[int] = None):
+                 group=None, host_exchange: bool = False, pieces: Optional[int] = None,
+                 col_pieces: Optional[int] = None):
         """host_exchange: stage the all-to-all through host memory over a gloo group (rehearsing
         several ranks on ONE GPU, where RCCL refuses duplicate devices); never the product path.
-        pieces: row pieces of the pipelined exchange (None: auto_pieces of the local share)."""
+        pieces / col_pieces: row / column pieces of the pipelined exchange (None: auto_pieces of the
+        local share: >= 2^22 elements per row piece, >= 2^21 per column piece, at most 4 of those)."""
         import torch.distributed as dist
         self.dist = dist
         self.group = group
@@ -295,9 +363,11 @@ class DistNTT:
         self.field_id, self.log_n, self.limbs64 = field_id, log_n, limbs64
         self.engine = RankPlan(field_id, log_n, limbs64, world, rank, device)
         self.layout = self.engine.layout
-        if pieces is None:  # world 1: no exchange to hide
-            pieces = 1 if world == 1 else self.auto_pieces(self.layout.local_n)
-        self.fs = FourStep(self.layout, self.engine, self, pieces=pieces)
+        ln = self.layout.local_n  # world 1: no exchange to hide
+        auto_r = 1 if world == 1 else self.auto_pieces(ln)
+        auto_c = 1 if world == 1 else self.auto_pieces(ln, cap=4, min_elems=self.MIN_COL_PIECE_ELEMS)
+        self.fs = FourStep(self.layout, self.engine, self, pieces=auto_r if pieces is None else pieces,
+                           col_pieces=auto_c if col_pieces is None else col_pieces)
         self.n = self.layout.n
         self.passes: List[int] = []  # per-transform schedules: see the row / column plans
         # exchange timing (set_profiling): one window per all-to-all, from the first piece's start to
@@ -310,8 +380,8 @@ class DistNTT:
     # tests/test_gpu_fullsize.py): larger per-peer runs go as several all-to-alls.
     MAX_PEER_BYTES = 1 << 30
 
-    # ---- FourStep exchange interface: rows [row0, row0 + nrows) of every peer chunk
-    def start(self, send, recv, nvec, row0, nrows):
+    # ---- FourStep exchange interface: runs of every peer block
+    def start(self, send, recv, peer_stride, runs):
         L = self.layout
         if self._x_windows is not None and (self._x_open is None or self._x_open[1] is not None):
             if self._x_open is not None:
@@ -319,12 +389,12 @@ class DistNTT:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record()
             self._x_open = [e0, None]
-        sv = piece_views(send, L.world, nvec, L.r, L.c, row0, nrows)
-        rv = piece_views(recv, L.world, nvec, L.r, L.c, row0, nrows)
+        sv = run_views(send, L.world, peer_stride, runs)
+        rv = run_views(recv, L.world, peer_stride, runs)
         works = []
-        for v in range(nvec):
-            ins = [sv[g][v] for g in range(L.world)]
-            outs = [rv[g][v] for g in range(L.world)]
+        for u in range(len(runs)):
+            ins = [sv[g][u] for g in range(L.world)]
+            outs = [rv[g][u] for g in range(L.world)]
             if self.host_exchange:
                 hr = torch.empty((L.world * ins[0].shape[0],) + tuple(ins[0].shape[1:]), dtype=ins[0].dtype)
                 self.dist.all_to_all_single(hr, torch.cat(ins).cpu(), group=self.group)
@@ -391,41 +461,76 @@ class DistNTT:
         return self.engine.last_launch_ms(0) + self.engine.last_launch_ms(1)
 
 
+class _RankList:
+    """G rank plans driven as one FourStep engine: every argument is a list with one tensor per rank
+    (y may be None), so the schedule interleaves the G ranks step by step on the current stream."""
+
+    def __init__(self, engines):
+        self.engines = engines
+
+    def empty(self, count):
+        return [e.empty(count) for e in self.engines]
+
+    def forward_rows_piece(self, x, send, nvec, slot, i, rp, cp):
+        for e, xg, sg in zip(self.engines, x, send):
+            e.forward_rows_piece(xg, sg, nvec, slot, i, rp, cp)
+
+    def forward_cols_piece(self, recv, x, nvec, slot, k, rp, cp):
+        for e, rg, xg in zip(self.engines, recv, x):
+            e.forward_cols_piece(rg, xg, nvec, slot, k, rp, cp)
+
+    def inverse_cols_piece(self, x, y, send, k, rp, cp):
+        for g, e in enumerate(self.engines):
+            e.inverse_cols_piece(x[g], None if y is None else y[g], send[g], k, rp, cp)
+
+    def inverse_rows_piece(self, recv, out, i, rp, cp):
+        for e, rg, og in zip(self.engines, recv, out):
+            e.inverse_rows_piece(rg, og, i, rp, cp)
+
+
 class VirtualRanks:
     """G ranks of the four-step in ONE process on one GPU; the all-to-all is device copies.
 
-    SURVEY §4: validate the distributed decomposition on a single GPU before RCCL.  With ``pieces``
-    > 1 the copies of each row piece run on a side stream while the next piece's row transforms run
-    (the schedule of FourStep, interleaved over the G ranks).
+    SURVEY §4: validate the distributed decomposition on a single GPU before RCCL.  The schedule is
+    FourStep's, over all G ranks at once; with pieces > 1 each exchange unit's copies run on a side
+    stream while the next piece's transforms run.
     """
 
-    def __init__(self, field_id: int, log_n: int, limbs64: int, world: int, device: int = 0, pieces: int = 1):
+    def __init__(self, field_id: int, log_n: int, limbs64: int, world: int, device: int = 0, pieces: int = 1,
+                 col_pieces: Optional[int] = None):
+        """col_pieces: column pieces (None: as many as row pieces)."""
         self.world = world
         self.engines = [RankPlan(field_id, log_n, limbs64, world, g, device) for g in range(world)]
-        self.ranks = [FourStep(e.layout, e, pieces=pieces) for e in self.engines]
-        self.layout0 = self.ranks[0].L
-        self.pieces = self.ranks[0].pieces
+        self.layout0 = self.engines[0].layout
+        self.layouts = [e.layout for e in self.engines]
+        self.fs = FourStep(self.layout0, _RankList(self.engines), self, pieces=pieces,
+                           col_pieces=pieces if col_pieces is None else col_pieces)
+        self.pieces = self.fs.pieces
         self.side = torch.cuda.Stream(device=device)
 
-    def _copy_piece(self, sends, recvs, nvec, row0, nrows):
-        """Rows [row0, row0 + nrows) of every (src -> dst) chunk, on the side stream after the work
-        enqueued so far; returns the event that marks their arrival."""
-        L, G = self.layout0, self.world
+    # ---- FourStep exchange interface over the G ranks' buffers (lists)
+    def start(self, sends, recvs, peer_stride, runs):
+        """Runs of every (src -> dst) block, on the side stream after the work enqueued so far; returns
+        the event that marks their arrival."""
+        G = self.world
         ev = torch.cuda.Event()
         ev.record()
         self.side.wait_event(ev)
         with torch.cuda.stream(self.side):
-            sv = [piece_views(t, G, nvec, L.r, L.c, row0, nrows) for t in sends]
-            rv = [piece_views(t, G, nvec, L.r, L.c, row0, nrows) for t in recvs]
+            sv = [run_views(t, G, peer_stride, runs) for t in sends]
+            rv = [run_views(t, G, peer_stride, runs) for t in recvs]
             for dst in range(G):
                 for src in range(G):
-                    for v in range(nvec):
-                        rv[dst][src][v].copy_(sv[src][dst][v])
+                    for u in range(len(runs)):
+                        rv[dst][src][u].copy_(sv[src][dst][u])
             done = torch.cuda.Event()
             done.record()
         for t in list(sends) + list(recvs):  # the side stream uses them: keep the caching allocator honest
             t.record_stream(self.side)
         return done
+
+    def wait(self, ev):
+        torch.cuda.current_stream().wait_event(ev)
 
     def empty(self) -> List[torch.Tensor]:
         return [e.empty(self.layout0.local_n) for e in self.engines]
@@ -436,51 +541,15 @@ class VirtualRanks:
         return xs
 
     def forward(self, xs: List[torch.Tensor]):
-        evs = []
-        for i, (a0, ra) in enumerate(self.pieces):
-            for fs, x in zip(self.ranks, xs):
-                fs.forward_rows_piece(x, i)
-            evs.append(self._copy_piece([fs.send for fs in self.ranks], [fs.recv for fs in self.ranks], 1, a0, ra))
-        for ev in evs:
-            torch.cuda.current_stream().wait_event(ev)
-        for fs, x in zip(self.ranks, xs):
-            fs.eng.forward_cols(fs.recv, x, 1, 0)
-        return xs
-
-    def _inverse_tail(self, outs):
-        evs = [self._copy_piece([fs.send for fs in self.ranks], [fs.recv for fs in self.ranks], 1, a0, ra)
-               for a0, ra in self.pieces]
-        for i, ev in enumerate(evs):
-            torch.cuda.current_stream().wait_event(ev)
-            for fs, o in zip(self.ranks, outs):
-                fs.inverse_rows_piece(o, i)
-        return outs
+        return self.fs.forward(xs)
 
     def inverse(self, xs: List[torch.Tensor]):
-        for fs, x in zip(self.ranks, xs):
-            fs.eng.inverse_cols(x, None, fs.send)
-        return self._inverse_tail(xs)
+        return self.fs.inverse(xs)
 
     def polymul(self, As: List[torch.Tensor], Bs: List[torch.Tensor], Outs: List[torch.Tensor]):
         if all(a is b for a, b in zip(As, Bs)):
-            self.forward(As)
-        else:
-            pairs = [fs.pair_buffers() for fs in self.ranks]
-            sends, recvs = [p[0] for p in pairs], [p[1] for p in pairs]
-            evs = []
-            for i, (a0, ra) in enumerate(self.pieces):
-                for g, fs in enumerate(self.ranks):
-                    fs.forward_rows_piece(As[g], i, 2, 0, sends[g])
-                    fs.forward_rows_piece(Bs[g], i, 2, 1, sends[g])
-                evs.append(self._copy_piece(sends, recvs, 2, a0, ra))
-            for ev in evs:
-                torch.cuda.current_stream().wait_event(ev)
-            for g, fs in enumerate(self.ranks):
-                fs.eng.forward_cols(recvs[g], As[g], 2, 0)
-                fs.eng.forward_cols(recvs[g], Bs[g], 2, 1)
-        for fs, a, b in zip(self.ranks, As, Bs):
-            fs.eng.inverse_cols(a, b, fs.send)
-        return self._inverse_tail(Outs)
+            Bs = As  # squaring: one forward, single-vector exchange
+        return self.fs.polymul(As, Bs, Outs)
 
 
 class MultiPlan:

@@ -80,6 +80,10 @@ PROTOTYPES = {
     "ntt_rplan_inverse_rows": (C.c_int, [_vp, _vp, _vp, _vp]),
     "ntt_rplan_forward_rows_range": (C.c_int, [_vp, _vp, _vp, C.c_uint, C.c_uint, C.c_uint64, C.c_uint64, _vp]),
     "ntt_rplan_inverse_rows_range": (C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, _vp]),
+    "ntt_rplan_forward_rows_piece": (C.c_int, [_vp, _vp, _vp, C.c_uint, C.c_uint, C.c_uint, C.c_uint, C.c_uint, _vp]),
+    "ntt_rplan_forward_cols_piece": (C.c_int, [_vp, _vp, _vp, C.c_uint, C.c_uint, C.c_uint, C.c_uint, C.c_uint, _vp]),
+    "ntt_rplan_inverse_cols_piece": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint, C.c_uint, C.c_uint, _vp]),
+    "ntt_rplan_inverse_rows_piece": (C.c_int, [_vp, _vp, _vp, C.c_uint, C.c_uint, C.c_uint, _vp]),
     "ntt_rplan_fill": (C.c_int, [_vp, _vp, C.c_int, C.c_uint64, _vp]),
     "ntt_rplan_set_profiling": (C.c_int, [_vp, C.c_int]),
     "ntt_rplan_last_launch_ms": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_float), C.c_uint, C.POINTER(C.c_uint)]),

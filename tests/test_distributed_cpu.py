@@ -21,18 +21,18 @@ def _free_port():
     return port
 
 
-def _exchange(layout, pieces):
-    """Whole-chunk all-to-all (plain callable, one piece) or the row-piece exchange interface."""
+def _exchange(layout, pieces, col_pieces=1):
+    """Whole-block all-to-all (plain callable, one piece) or the piece exchange interface."""
     from tests.dist_helpers import GlooPieceExchange
-    if pieces == 1:
+    if pieces == 1 and col_pieces == 1:
         return lambda s, r: dist.all_to_all_single(r.view(-1), s.view(-1))
     return GlooPieceExchange(layout)
 
 
-def _worker(rank, world, port, field_id, log_n, L, q, pieces=1, log_n2=None):
+def _worker(rank, world, port, field_id, log_n, L, q, pieces=1, log_n2=None, col_pieces=1):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    from ntt_amd.distributed import FourStep, Layout
+    from ntt_amd.distributed import FourStep, Layout, pow2_pieces
     from tests.dist_helpers import CpuOracleEngine, row_shares
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -43,8 +43,8 @@ def _worker(rank, world, port, field_id, log_n, L, q, pieces=1, log_n2=None):
         share = row_shares(x, Layout, log_n, world, L, log_n2)[rank]
         eng = CpuOracleEngine(field_id, log_n, L, world, rank, log_n2)
         lay = Layout(log_n, world, rank, log_n2)
-        fs = FourStep(lay, eng, _exchange(lay, pieces), pieces=pieces)
-        assert len(fs.pieces) == min(pieces, lay.r)
+        fs = FourStep(lay, eng, _exchange(lay, pieces, col_pieces), pieces=pieces, col_pieces=col_pieces)
+        assert len(fs.pieces) == pow2_pieces(pieces, lay.r) and fs.cp == pow2_pieces(col_pieces, lay.c)
         fs.forward(share)
         fwd = share.clone()
         fs.inverse(share)
@@ -55,21 +55,24 @@ def _worker(rank, world, port, field_id, log_n, L, q, pieces=1, log_n2=None):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,field_id,log_n,pieces,log_n2", [(2, 1, 6, 1, None), (2, 2, 7, 1, None),
-                                                                 (4, 1, 8, 1, None), (2, 1, 6, 2, None),
-                                                                 (2, 2, 7, 3, None), (4, 1, 8, 4, None),
-                                                                 (2, 1, 8, 2, 3), (4, 2, 9, 1, 3)])
-def test_four_step_gloo(world, field_id, log_n, pieces, log_n2):
-    """pieces > 1: the pipelined schedule (row transforms and the all-to-all in row pieces, uneven
-    last piece included) gives the same column layout and round trip.  log_n2: an unbalanced split
-    n1 > n2 (what the rank plans pick when it saves a pass, ntt_rplan.cpp choose_split)."""
+@pytest.mark.parametrize("world,field_id,log_n,pieces,log_n2,col_pieces",
+                         [(2, 1, 6, 1, None, 1), (2, 2, 7, 1, None, 1), (4, 1, 8, 1, None, 1), (2, 1, 6, 2, None, 1),
+                          (2, 2, 7, 3, None, 1), (4, 1, 8, 4, None, 1), (2, 1, 8, 2, 3, 1), (4, 2, 9, 1, 3, 1),
+                          (2, 1, 8, 1, None, 4), (2, 1, 8, 2, None, 2), (4, 1, 10, 4, None, 2),
+                          (2, 2, 9, 4, 4, 8)])
+def test_four_step_gloo(world, field_id, log_n, pieces, log_n2, col_pieces):
+    """pieces / col_pieces > 1: the pipelined schedule (the all-to-all in row-piece x column-piece
+    units overlapping the row transforms before it and the column transforms after it; a count that
+    is not a power of two rounds down) gives the same column layout and round trip.  log_n2: an
+    unbalanced split n1 > n2 (what the rank plans pick when it saves a pass, ntt_rplan.cpp
+    choose_split)."""
     from ntt_amd.distributed import Layout
     from tests.dist_helpers import gather_cols
     L = 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, field_id, log_n, L, q, pieces, log_n2))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, field_id, log_n, L, q, pieces, log_n2, col_pieces))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -111,7 +114,7 @@ def test_layout_rejects_bad_world():
         Layout(10, 8, 0, 2)  # fewer columns than ranks
 
 
-def _polymul_worker(rank, world, port, field_id, log_n, L, square, q, pieces=1, log_n2=None):
+def _polymul_worker(rank, world, port, field_id, log_n, L, square, q, pieces=1, log_n2=None, col_pieces=1):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from ntt_amd.distributed import FourStep, Layout
@@ -128,21 +131,18 @@ def _polymul_worker(rank, world, port, field_id, log_n, L, square, q, pieces=1, 
         out = torch.zeros_like(sa)
         eng = CpuOracleEngine(field_id, log_n, L, world, rank, log_n2)
         lay = Layout(log_n, world, rank, log_n2)
-        fs = FourStep(lay, eng, _exchange(lay, pieces), pieces=pieces)
+        fs = FourStep(lay, eng, _exchange(lay, pieces, col_pieces), pieces=pieces, col_pieces=col_pieces)
         fs.polymul(sa, sb, out)
         q.put((rank, out.numpy().tobytes()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,field_id,log_n,square,pieces,log_n2", [(2, 1, 6, False, 1, None),
-                                                                        (4, 1, 8, False, 1, None),
-                                                                        (2, 2, 7, True, 1, None),
-                                                                        (2, 1, 6, False, 2, None),
-                                                                        (4, 1, 8, False, 4, None),
-                                                                        (2, 2, 7, True, 2, None),
-                                                                        (2, 1, 8, False, 2, 3)])
-def test_distributed_polymul_gloo(world, field_id, log_n, square, pieces, log_n2):
+@pytest.mark.parametrize("world,field_id,log_n,square,pieces,log_n2,col_pieces",
+                         [(2, 1, 6, False, 1, None, 1), (4, 1, 8, False, 1, None, 1), (2, 2, 7, True, 1, None, 1),
+                          (2, 1, 6, False, 2, None, 1), (4, 1, 8, False, 4, None, 1), (2, 2, 7, True, 2, None, 1),
+                          (2, 1, 8, False, 2, 3, 1), (2, 1, 8, False, 2, None, 4), (4, 2, 10, True, 2, None, 2)])
+def test_distributed_polymul_gloo(world, field_id, log_n, square, pieces, log_n2, col_pieces):
     """C5's schedule (forward(a), forward(b) in ONE all-to-all, local pointwise product fused into
     the inverse, inverse all-to-all) over gloo: the row-layout result equals the oracle's cyclic
     product; squaring (a is b) takes the single-vector exchange."""
@@ -152,7 +152,8 @@ def test_distributed_polymul_gloo(world, field_id, log_n, square, pieces, log_n2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_polymul_worker, args=(r, world, port, field_id, log_n, L, square, q, pieces, log_n2))
+    procs = [ctx.Process(target=_polymul_worker,
+                         args=(r, world, port, field_id, log_n, L, square, q, pieces, log_n2, col_pieces))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -178,9 +179,12 @@ def test_distributed_polymul_gloo(world, field_id, log_n, square, pieces, log_n2
 
 
 def test_piece_ranges_and_auto_pieces():
-    """Row pieces tile [0, r) exactly (uneven last piece allowed); the automatic count keeps every
-    piece's row transforms >= 2^22 elements (full GPU launches) and never exceeds the cap."""
-    from ntt_amd.distributed import DistNTT, FourStep
+    """Row ranges tile [0, r) exactly (uneven last piece allowed; the row-range entry points); the
+    schedule's piece counts are powers of two <= the rows / columns; the automatic count keeps every
+    piece's transforms >= 2^22 elements (full GPU launches) and never exceeds the cap."""
+    from ntt_amd.distributed import DistNTT, FourStep, pow2_pieces
+    assert [pow2_pieces(k, 8) for k in (0, 1, 2, 3, 4, 5, 7, 8, 9, 100)] == [1, 1, 2, 2, 4, 4, 4, 8, 8, 8]
+    assert pow2_pieces(8, 2) == 2 and pow2_pieces(3, 1) == 1
     for r in (1, 2, 3, 4, 7, 512, 2048):
         for k in (1, 2, 3, 4, 8, 100):
             pr = FourStep.piece_ranges(r, k)
@@ -193,3 +197,8 @@ def test_piece_ranges_and_auto_pieces():
     for ln in range(10, 32):
         k = DistNTT.auto_pieces(1 << ln)
         assert k == 1 or (1 << ln) // k >= DistNTT.MIN_PIECE_ELEMS
+        kc = DistNTT.auto_pieces(1 << ln, cap=4, min_elems=DistNTT.MIN_COL_PIECE_ELEMS)
+        assert kc <= 4 and (kc == 1 or (1 << ln) // kc >= DistNTT.MIN_COL_PIECE_ELEMS)
+    # 2^24 over 2 GPUs (2^23 per rank): 2 row pieces, 4 column pieces; over 8 (2^21): none
+    assert DistNTT.auto_pieces(1 << 23, cap=4, min_elems=DistNTT.MIN_COL_PIECE_ELEMS) == 4
+    assert DistNTT.auto_pieces(1 << 21, cap=4, min_elems=DistNTT.MIN_COL_PIECE_ELEMS) == 1

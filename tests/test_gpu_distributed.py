@@ -29,17 +29,20 @@ def _eq_at(t, src, idx, chunk=1 << 22):
     return all(torch.equal(t[i:i + chunk], src[idx[i:i + chunk]]) for i in range(0, idx.numel(), chunk))
 
 
-@pytest.mark.parametrize("world,log_n,field_id,L,pieces", [(1, 12, 1, 4, 1), (2, 12, 1, 4, 1), (4, 16, 1, 4, 1),
-                                                            (8, 20, 1, 4, 1), (8, 16, 2, 6, 1), (2, 14, 0, 1, 1),
-                                                            (2, 12, 1, 4, 4), (8, 20, 1, 4, 4), (4, 16, 1, 4, 3),
-                                                            (8, 16, 2, 6, 2), (2, 14, 0, 1, 8),
-                                                            (1, 22, 1, 4, 1), (4, 22, 1, 4, 2), (8, 24, 1, 4, 1),
-                                                            (2, 22, 2, 6, 1), (1, 26, 1, 4, 1)])
-def test_virtual_ranks_match_single_gpu(world, log_n, field_id, L, pieces):
-    """pieces > 1: the pipelined schedule (row pieces exchanged on a side stream while the next
-    piece is transformed) -- same column layout, same round trip.  2^22 / 2^24 / 2^26: the rank
-    plans' unbalanced split (n2 = 2^10, one workgroup tile per row transform); 2^26 at world 1 has
-    2^16 rows per rank, launched in chunks of 2^15 (grid.y)."""
+@pytest.mark.parametrize("world,log_n,field_id,L,pieces,col_pieces",
+                         [(1, 12, 1, 4, 1, 1), (2, 12, 1, 4, 1, 1), (4, 16, 1, 4, 1, 1), (8, 20, 1, 4, 1, 1),
+                          (8, 16, 2, 6, 1, 1), (2, 14, 0, 1, 1, 1), (2, 12, 1, 4, 4, 1), (8, 20, 1, 4, 4, 1),
+                          (4, 16, 1, 4, 3, 1), (8, 16, 2, 6, 2, 1), (2, 14, 0, 1, 8, 1), (1, 22, 1, 4, 1, 1),
+                          (4, 22, 1, 4, 2, 1), (8, 24, 1, 4, 1, 1), (2, 22, 2, 6, 1, 1), (1, 26, 1, 4, 1, 1),
+                          (2, 12, 1, 4, 1, 4), (2, 12, 1, 4, 4, 4), (8, 20, 1, 4, 4, 4), (4, 16, 1, 4, 2, 8),
+                          (2, 14, 0, 1, 2, 2), (8, 16, 2, 6, 2, 2), (4, 22, 1, 4, 4, 4), (2, 24, 1, 4, 2, 2),
+                          (1, 26, 1, 4, 4, 8)])
+def test_virtual_ranks_match_single_gpu(world, log_n, field_id, L, pieces, col_pieces):
+    """pieces / col_pieces > 1: the pipelined schedule (the exchange units copied on a side stream
+    while the row transforms before them and the column transforms after them run) -- same column
+    layout, same round trip.  2^22 / 2^24 / 2^26: the rank plans' unbalanced split (n2 = 2^10, one
+    workgroup tile per row transform); 2^26 at world 1 has 2^16 rows per rank, launched in chunks of
+    2^15 (grid.y)."""
     from ntt_amd.distributed import VirtualRanks
     from ntt_amd.ntt import NTTPlan
     ref = NTTPlan(field_id, log_n, L)
@@ -47,14 +50,14 @@ def test_virtual_ranks_match_single_gpu(world, log_n, field_id, L, pieces):
     ref.fill(x, "random", seed=42)
     x0 = x.clone()
     ref.forward(x)
-    vr = VirtualRanks(field_id, log_n, L, world, pieces=pieces)
+    vr = VirtualRanks(field_id, log_n, L, world, pieces=pieces, col_pieces=col_pieces)
     xs = vr.fill(vr.empty(), "random", seed=42)
-    for fs, t in zip(vr.ranks, xs):  # row-layout shares hold the right global elements
-        assert _eq_at(t, x0, _index(fs.L, "row"))
+    for lay, t in zip(vr.layouts, xs):  # row-layout shares hold the right global elements
+        assert _eq_at(t, x0, _index(lay, "row"))
     shares = [t.clone() for t in xs]
     vr.forward(xs)
-    for fs, t in zip(vr.ranks, xs):
-        assert _eq_at(t, x, _index(fs.L, "col")), (world, log_n, fs.L.rank)
+    for lay, t in zip(vr.layouts, xs):
+        assert _eq_at(t, x, _index(lay, "col")), (world, log_n, lay.rank)
     vr.inverse(xs)
     for s, t in zip(shares, xs):
         assert torch.equal(s, t)
@@ -72,8 +75,9 @@ def test_rank_plan_split_takes_fewest_passes():
 
 
 def test_dist_ntt_rccl_world1():
-    """DistNTT over a real RCCL group (world size 1): whole-chunk exchange, and the pipelined
-    exchange (async RCCL all-to-all per row piece, uneven last piece) forced on."""
+    """DistNTT over a real RCCL group (world size 1): whole-block exchange, and the pipelined
+    exchange (async RCCL all-to-all per unit; 3 rounds down to 2 pieces) forced on, on one side and
+    on both."""
     import torch.distributed as dist
     from ntt_amd.distributed import DistNTT
     from ntt_amd.ntt import NTTPlan
@@ -85,9 +89,10 @@ def test_dist_ntt_rccl_world1():
         ref = NTTPlan(1, log_n, 4)
         x = ref.fill(ref.empty(), "random", seed=3)
         ref.forward(x)
-        for pieces in (None, 4, 3):
-            d = DistNTT(1, log_n, 4, device=0, pieces=pieces)
-            assert len(d.fs.pieces) == (1 if pieces is None else pieces)
+        for pieces, col_pieces in ((None, None), (4, 1), (3, 1), (1, 4), (4, 8)):
+            d = DistNTT(1, log_n, 4, device=0, pieces=pieces, col_pieces=col_pieces)
+            assert len(d.fs.pieces) == {None: 1, 4: 4, 3: 2, 1: 1}[pieces]
+            assert d.fs.cp == (1 if col_pieces is None else col_pieces)
             t = d.fill(d.empty(), "random", seed=3)
             t0 = t.clone()
             d.forward(t)

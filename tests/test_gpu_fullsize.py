@@ -89,10 +89,10 @@ def test_c4_fourstep_2pow28_eight_virtual_ranks():
     vr.forward(xs)
     rng = np.random.default_rng(4)
     ks = [0, 1, 2, 3, n // 2, n - 1] + [int(k) for k in rng.integers(0, n, 30)]
-    _kat_check_columns(xs, [fs.L for fs in vr.ranks], n, p, g, L, ks)
+    _kat_check_columns(xs, vr.layouts, n, p, g, L, ks)
     vr.inverse(xs)
-    for fs, t in zip(vr.ranks, xs):
-        assert torch.equal(t[:, 0], _row_index(fs.L, t.device)) and not bool(t[:, 1:].any()), fs.L.rank
+    for lay, t in zip(vr.layouts, xs):
+        assert torch.equal(t[:, 0], _row_index(lay, t.device)) and not bool(t[:, 1:].any()), lay.rank
 
 
 @pytest.mark.parametrize("log_n", [26, 28])

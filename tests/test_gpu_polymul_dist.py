@@ -65,8 +65,13 @@ def _single_gpu_product(fid, L, log_n, seed_a, seed_b):
                                                              (4, 1, 4, 16, False, 1), (8, 1, 4, 20, False, 1),
                                                              (8, 2, 6, 16, False, 1), (2, 0, 1, 14, False, 1),
                                                              (4, 1, 4, 14, True, 1), (4, 1, 4, 16, False, 4),
-                                                             (8, 2, 6, 16, False, 3), (4, 1, 4, 14, True, 2)])
+                                                             (8, 2, 6, 16, False, 3), (4, 1, 4, 14, True, 2),
+                                                             (2, 0, 1, 14, False, 2), (2, 1, 4, 12, False, 2),
+                                                             (2, 1, 4, 22, False, 4)])
 def test_virtual_ranks_polymul_matches_single_gpu(world, fid, L, log_n, square, pieces):
+    """pieces > 1: as many row and column pieces (VirtualRanks' default); the P field (no fused
+    product) and 2^12 over 2 (single-pass column transforms) take the gathered-product path of
+    ntt_rplan_inverse_cols_piece."""
     from ntt_amd.distributed import VirtualRanks
     exp = _single_gpu_product(fid, L, log_n, 5, None if square else 6)
     vr = VirtualRanks(fid, log_n, L, world, pieces=pieces)
@@ -74,8 +79,8 @@ def test_virtual_ranks_polymul_matches_single_gpu(world, fid, L, log_n, square, 
     Bs = As if square else vr.fill(vr.empty(), "random", seed=6)
     Outs = vr.empty()
     vr.polymul(As, Bs, Outs)
-    for fs, o in zip(vr.ranks, Outs):
-        assert torch.equal(o, exp[_row_index(fs.L, o.device)]), (world, log_n, fs.L.rank)
+    for lay, o in zip(vr.layouts, Outs):
+        assert torch.equal(o, exp[_row_index(lay, o.device)]), (world, log_n, lay.rank)
 
 
 def test_c5_polymul_2pow24_eight_virtual_ranks():
@@ -87,8 +92,8 @@ def test_c5_polymul_2pow24_eight_virtual_ranks():
     As = vr.fill(vr.empty(), "random", seed=5)
     Bs = vr.fill(vr.empty(), "random", seed=6)
     vr.polymul(As, Bs, As)  # out aliases a
-    for fs, o in zip(vr.ranks, As):
-        assert torch.equal(o, exp[_row_index(fs.L, o.device)]), fs.L.rank
+    for lay, o in zip(vr.layouts, As):
+        assert torch.equal(o, exp[_row_index(lay, o.device)]), lay.rank
 
 
 @pytest.mark.parametrize("log_n,pieces", [(16, None), (24, None), (16, 4), (24, 8)])
@@ -141,12 +146,13 @@ def test_dist_ntt_polymul_rccl_world1():
     try:
         log_n = 18
         exp = _single_gpu_product(1, 4, log_n, 5, 6)
-        for pieces in (None, 4):  # whole chunks; pipelined async RCCL pieces (a and b in each piece)
-            d = DistNTT(1, log_n, 4, device=0, pieces=pieces)
+        # whole blocks; pipelined async RCCL units (a and b in each), row pieces only and both sides
+        for pieces, col_pieces in ((None, None), (4, 1), (4, 4)):
+            d = DistNTT(1, log_n, 4, device=0, pieces=pieces, col_pieces=col_pieces)
             a = d.fill(d.empty(), "random", seed=5)
             b = d.fill(d.empty(), "random", seed=6)
             out = d.empty()
             d.polymul(a, b, out)
-            assert torch.equal(out, exp[_row_index(d.layout, "cuda:0")]), pieces
+            assert torch.equal(out, exp[_row_index(d.layout, "cuda:0")]), (pieces, col_pieces)
     finally:
         dist.destroy_process_group()

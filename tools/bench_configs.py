@@ -93,13 +93,14 @@ def main():
              timeit(lambda: pl.forward(t), w, s), passes=pl.passes)
         del pl, t
         torch.cuda.empty_cache()
-    for pieces in (1, 4):
-        vr = VirtualRanks(1, 28, 4, 8, pieces=pieces)
+    for pieces, cpieces in ((1, 1), (4, 1), (4, 4)):
+        vr = VirtualRanks(1, 28, 4, 8, pieces=pieces, col_pieces=cpieces)
         xs = vr.fill(vr.empty(), "random", seed=4)
-        emit(f"C4: 2^28 forward BN254 Fr, four-step over 8 virtual ranks on one GPU, {pieces} exchange piece(s)",
-             1 << 28, timeit(lambda: vr.forward(xs), 2, 3), pieces=pieces,
-             note="exchange = device copies on one GPU (side stream, overlapping the row transforms when "
-                  "pieces > 1); the RCCL all-to-all is timed by bench.py --four-step")
+        emit(f"C4: 2^28 forward BN254 Fr, four-step over 8 virtual ranks on one GPU, {pieces} x {cpieces} "
+             f"exchange piece(s)", 1 << 28, timeit(lambda: vr.forward(xs), 2, 3), pieces=pieces, col_pieces=cpieces,
+             note="exchange = device copies on one GPU (side stream, overlapping the row transforms before it "
+                  "and the column transforms after it when pieces > 1); the RCCL all-to-all is timed by "
+                  "bench.py --four-step")
         del vr, xs
         torch.cuda.empty_cache()
 
@@ -126,12 +127,13 @@ def main():
     del pl, a, b, c
     torch.cuda.empty_cache()
     for pieces in (1, 4):
-        vr = VirtualRanks(1, 24, 4, 8, pieces=pieces)
+        vr = VirtualRanks(1, 24, 4, 8, pieces=pieces, col_pieces=pieces)
         As = vr.fill(vr.empty(), "random", seed=5)
         Bs = vr.fill(vr.empty(), "random", seed=6)
         Cs = vr.empty()
         emit(f"C5: polymul length 2^24 BN254 Fr, distributed schedule over 8 virtual ranks on one GPU, "
-             f"{pieces} exchange piece(s)", 1 << 24, timeit(lambda: vr.polymul(As, Bs, Cs), 5, 10), pieces=pieces,
+             f"{pieces} x {pieces} exchange piece(s)", 1 << 24, timeit(lambda: vr.polymul(As, Bs, Cs), 5, 10),
+             pieces=pieces,
              note="2 exchanges (a and b batched in one) as device copies; RCCL timing needs a multi-GPU node")
         del vr, As, Bs, Cs
         torch.cuda.empty_cache()

@@ -26,8 +26,8 @@ def main():
     xs = vr.fill(vr.empty(), "random", seed=9)
     vr.forward(xs)
     ok = True
-    for fs, t in zip(vr.ranks, xs):
-        L = fs.L
+    for lay, t in zip(vr.layouts, xs):
+        L = lay
         i = torch.arange(L.local_n, dtype=torch.int64, device="cuda:0")
         idx = L.rank * L.c + (i & (L.c - 1)) + L.n2 * (i >> L.log_c)
         ok = ok and torch.equal(t, x[idx])
