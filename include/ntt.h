@@ -88,9 +88,11 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
  * GZKP-NTT.cu:1359-1449): the plan owns no n-element buffer.  The radices are arranged as a
  * palindrome (R_1 = R_p, middle radices symmetric; one pass more than the default schedule when
  * log_n admits no palindrome of that length, e.g. odd log_n over an even pass count), every pass
- * writes the positions it read, and the digit reversal is a final pass of disjoint tile-pair swaps
- * (the permutation is an involution).  Same contract and results as the default schedule; one more
- * read + write of the vector.  P469762049 plans run on 8-B scratch elements for it (the default P
+ * writes the positions it read, and the digit reversal (an involution) is fused into the final
+ * pass: each final tile writes natural positions once the mirror slab has been read (k_final_ipn,
+ * bounded waits reported by ntt_plan_device_status); batched calls take a separate pass of disjoint
+ * tile-pair swaps instead.  Same contract and results as the default schedule, within ~1 % of its
+ * time on the 256-bit path.  P469762049 plans run on 8-B scratch elements for it (the default P
  * plan keeps 4-B ones).  The 6-limb 256-bit layout (48-B elements, 32-B scratch), sizes with no
  * palindrome the pass kernels accept (2^11 and 2^13 on the 1024-element tiles; P: 2^15, 2^17, 2^19
  * on its 8192-element tiles) and the rival schedules return NTT_ERR_ARG. */
@@ -103,8 +105,15 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
  * reports a dependency wait that gave up (a watchdog; never expected). */
 #define NTT_PLAN_SINGLE_LAUNCH 32u
 int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags);
-/* Watchdog of NTT_PLAN_SINGLE_LAUNCH: *bad = non-zero if a launch since the last call had a tile
- * give up waiting for its inputs (its output is then wrong).  Blocking; clears the word. */
+/* Device-side status of a plan since the last call (blocking; clears it).  *bad bit 0: an
+ * inter-workgroup wait gave up at its watchdog (NTT_PLAN_SINGLE_LAUNCH, or the fused digit reversal
+ * of NTT_PLAN_IN_PLACE): that call's output is wrong.  The checked build (ntt_amd/libntt_debug.so,
+ * same ABI, `python -m ntt_amd.build --debug`) adds, from checks inside every pass kernel:
+ *   0x100  an element index outside its buffer (the access went to element 0 instead)
+ *   0x200  a caller input element >= p (the inputs must be canonical, as in the reference)
+ *   0x400  an intermediate >= 2p (a lazy-reduction bound broke)
+ *   0x800  an output element >= p
+ * The product build never sets these bits. */
 int ntt_plan_device_status(ntt_plan* plan, unsigned* bad);
 
 /* Modulus-generic plan, like big-num.cu's `prime` / `omega` kernel arguments (big-num.cu:68,173,260):

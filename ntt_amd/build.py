@@ -14,12 +14,20 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-# Experiment variants (never the default product): NTT_BUILD_TAG=<tag> NTT_BUILD_DEFINES="-DX=1 ..."
-# builds ntt_amd/libntt_<tag>.so from ntt_amd/_build_<tag>/; NTT_LIB_PATH selects it at load time.
+# Variants beside the product: NTT_BUILD_TAG=<tag> NTT_BUILD_DEFINES="-DX=1 ..." builds
+# ntt_amd/libntt_<tag>.so from ntt_amd/_build_<tag>/ (experiments); NTT_LIB_PATH selects it at load
+# time.  build_debug() is the checked build (NTT_DEBUG_CHECKS, libntt_debug.so).
 _TAG = os.environ.get("NTT_BUILD_TAG", "")
 _DEFINES = os.environ.get("NTT_BUILD_DEFINES", "").split()
-BUILD = os.path.join(HERE, "_build" + (f"_{_TAG}" if _TAG else ""))
-LIB = os.path.join(HERE, "libntt" + (f"_{_TAG}" if _TAG else "") + ".so")
+
+
+def _paths(tag: str):
+    return (os.path.join(HERE, "_build" + (f"_{tag}" if tag else "")),
+            os.path.join(HERE, "libntt" + (f"_{tag}" if tag else "") + ".so"))
+
+
+BUILD, LIB = _paths(_TAG)
+DEBUG_LIB = _paths("debug")[1]
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
 # slowest translation units first (the pool runs them in list order)
@@ -62,13 +70,13 @@ def _deps() -> float:
     return latest
 
 
-def _compile(src: str, hdr_mtime: float) -> str:
+def _compile(src: str, hdr_mtime: float, build_dir: str, defines) -> str:
     s = os.path.join(CSRC, src)
-    o = os.path.join(BUILD, src + ".o")
+    o = os.path.join(build_dir, src + ".o")
     if os.path.exists(o) and os.path.getmtime(o) >= max(os.path.getmtime(s), hdr_mtime):
         return o
     cmd = [hipcc(), "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-c", s, "-o", o,
-           "-I", CSRC, "-I", INCLUDE, "-Wno-pass-failed", "-Wno-unused-command-line-argument", *_DEFINES]
+           "-I", CSRC, "-I", INCLUDE, "-Wno-pass-failed", "-Wno-unused-command-line-argument", *defines]
     if src.endswith(".cpp"):
         cmd[1:1] = ["-x", "hip"]
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -77,25 +85,39 @@ def _compile(src: str, hdr_mtime: float) -> str:
     return o
 
 
-def build(verbose: bool = False, jobs: int | None = None) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def build(verbose: bool = False, jobs: int | None = None, tag: str | None = None, defines=None) -> str:
+    """Build libntt.so (or the variant `tag` with extra -D `defines`; default: NTT_BUILD_TAG /
+    NTT_BUILD_DEFINES from the environment).  Incremental: objects newer than their sources stay."""
+    build_dir, lib = _paths(_TAG if tag is None else tag)
+    defines = _DEFINES if defines is None else list(defines)
+    os.makedirs(build_dir, exist_ok=True)
     hdr = _deps()
     srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
     jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 4)))
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, hdr), srcs))
-    if not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
-        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB + ".tmp", *objs]
+        objs = list(ex.map(lambda s: _compile(s, hdr, build_dir, defines), srcs))
+    if not os.path.exists(lib) or any(os.path.getmtime(o) > os.path.getmtime(lib) for o in objs):
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib + ".tmp", *objs]
         cmd += ["-ldl"]  # RCCL is dlopen-ed by ntt_multi.cpp at first multi-GPU use
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
-        os.replace(LIB + ".tmp", LIB)
+        os.replace(lib + ".tmp", lib)
     if verbose:
-        print(f"built {LIB}")
-    return LIB
+        print(f"built {lib}")
+    return lib
+
+
+def build_debug(verbose: bool = False, jobs: int | None = None) -> str:
+    """The checked build ntt_amd/libntt_debug.so (NTT_DEBUG_CHECKS=1: index bounds, canonical inputs
+    and outputs, lazy bounds inside the kernels; ntt_plan_device_status reports violations).  Same
+    C ABI; select it with NTT_LIB_PATH.  Slower: for debugging callers, never measured."""
+    return build(verbose, jobs, tag="debug", defines=["-DNTT_DEBUG_CHECKS=1"])
 
 
 if __name__ == "__main__":
-    build(verbose=True)
+    if "--debug" in sys.argv:
+        build_debug(verbose=True)
+    else:
+        build(verbose=True)
     sys.exit(0)

@@ -16,6 +16,22 @@
 #ifndef NTT_AB_SKIP
 #define NTT_AB_SKIP 0
 #endif
+// Debug build (ntt_amd/libntt_debug.so, NTT_DEBUG_CHECKS=1): the pass kernels check every HBM index
+// against its buffer, the caller's inputs for canonical form, the lazy bound (< 2p) of every
+// intermediate and the canonical form of every output, and record violations in a per-plan status
+// word that ntt_plan_device_status reports (bits below).  The product build compiles none of it.
+#ifndef NTT_DEBUG_CHECKS
+#define NTT_DEBUG_CHECKS 0
+#endif
+enum : uint32_t {
+  NTT_DBG_BOUNDS = 1u << 8,  // an element index outside its buffer (the access is redirected to element 0)
+  NTT_DBG_INPUT = 1u << 9,   // a caller input element >= p
+  NTT_DBG_LAZY = 1u << 10,   // an intermediate (plan scratch) >= 2p
+  NTT_DBG_OUTPUT = 1u << 11  // an output element >= p
+};
+__device__ __forceinline__ void ntt_dbg_flag(uint32_t* status, uint32_t bit) {
+  if (status) __hip_atomic_fetch_or(status, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 #ifndef NTT_WAVES_256
 #define NTT_WAVES_256 4
 #endif
@@ -38,6 +54,9 @@
 #endif
 #ifndef NTT_P_LDS_TW
 #define NTT_P_LDS_TW 1
+#endif
+#ifndef NTT_EPT_P
+#define NTT_EPT_P 8  // elements per thread of the P path (16: two radix-8 register groups per thread)
 #endif
 #ifndef NTT_TILE_LOG_P
 #define NTT_TILE_LOG_P 13
@@ -115,7 +134,19 @@ struct Eng29 {
     float red_inv;        // 1 / (p_top + 1) rounded down (quotient-estimate reduction)
     uint32_t red_ok;      // p_top >= 2^18: the top-limb quotient estimate is within 1
     uint32_t pc[5][L];    // padded offsets K p for the unnormalised butterflies (PC_* below)
+    uint32_t* dbg;        // debug builds: the plan's status word (NTT_DBG_*); null otherwise
   };
+  // debug builds: x < q (x any limb representation of a non-negative value, q normalised)
+  __device__ static bool dbg_below(const uint32_t (&x)[W], const uint32_t (&q)[L]) {
+    uint32_t y[W];
+#pragma unroll
+    for (int i = 0; i < W; ++i) y[i] = x[i];
+    norm_u<L>(y);
+    for (int i = L - 1; i >= 0; --i)
+      if (y[i] != q[i]) return y[i] < q[i];
+    return false;
+  }
+  __device__ static bool dbg_canonical(const uint32_t (&x)[W], const Args& A) { return dbg_below(x, A.kp[0]); }
   // Padded offsets: value K p, limbs c_0 = kp_0 + P, c_i = kp_i + P - P/2^29 (0 < i < 8),
   // c_8 = kp_8 - P/2^29, so that c_i >= P > b_i for limb bound P and a - b + C never goes negative
   // limb-wise; K = (value bound of b) + 1 keeps the top limb non-negative when p_top >= 3.
@@ -205,6 +236,9 @@ struct Eng29 {
   __device__ static __forceinline__ void store_lazy(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
                                                     const Args& A) {
     reduce<BOUND, 2, FAST>(x, A);
+#if NTT_DEBUG_CHECKS
+    if (!dbg_below(x, A.kp[1])) ntt_dbg_flag(A.dbg, NTT_DBG_LAZY);
+#endif
     put<MW, WT>(base, idx, x);
   }
   // x < BOUND p -> canonical -> HBM
@@ -212,6 +246,9 @@ struct Eng29 {
   __device__ static __forceinline__ void store(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
                                                const Args& A) {
     reduce<BOUND, 1, FAST>(x, A);
+#if NTT_DEBUG_CHECKS
+    if (!dbg_below(x, A.kp[0])) ntt_dbg_flag(A.dbg, NTT_DBG_OUTPUT);
+#endif
     put<MW>(base, idx, x);
   }
   template <int MW = W32, bool WT = false>
@@ -356,7 +393,7 @@ struct Eng32 {
   static constexpr int LDSW = 1;
   static constexpr int IN = 4;       // bound hints of the generic kernels (every value here is < 2p)
   static constexpr int MUL_OUT = 4;
-  static constexpr int EPT = 8;
+  static constexpr int EPT = NTT_EPT_P;
   // 8192-element tiles (32 KiB LDS, 1024 threads) and >= 16 columns per column-pass workgroup, so
   // every HBM run is >= 128 B; 2048-element tiles left 64-B runs at radix 256 and 32-B runs at
   // radix 512 (2.0-3.3 TB/s).
@@ -386,10 +423,12 @@ struct Eng32 {
     uint32_t pinv;   // p^-1 mod 2^32 (Montgomery products)
     Tw w8[3];        // w_8^1, w_8^2, w_8^3
     Tw ninv;         // n^-1
+    uint32_t* dbg;   // debug builds: the plan's status word (NTT_DBG_*); null otherwise
   };
   __device__ static __forceinline__ uint32_t red(uint32_t x, uint32_t m) {  // x < 2m -> x < m
     return min(x, x - m);
   }
+  __device__ static bool dbg_canonical(const uint32_t (&x)[W], const Args& A) { return x[0] < A.p; }
   __device__ static __forceinline__ uint32_t shoup(uint32_t x, uint32_t w, uint32_t ws, uint32_t p) {
     const uint32_t q = __umulhi(x, ws);
     return x * w - q * p;  // [0, 2p)
@@ -415,15 +454,22 @@ struct Eng32 {
   // scratch between passes: the lazy value (< 2p < 2^31)
   template <int BOUND, bool FAST = false, int MW = MEMW_, bool WT = false>
   __device__ static __forceinline__ void store_lazy(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
-                                                    const Args&) {
+                                                    [[maybe_unused]] const Args& A) {
     static_assert(!WT, "write-through scratch stores: Eng29 engines only (fused schedule)");
+#if NTT_DEBUG_CHECKS
+    if (x[0] >= A.p2) ntt_dbg_flag(A.dbg, NTT_DBG_LAZY);
+#endif
     put<MW>(base, idx, x[0]);
   }
   // canonical (< p)
   template <int BOUND, bool FAST = false, int MW = MEMW_>
   __device__ static __forceinline__ void store(uint32_t* __restrict__ base, size_t idx, uint32_t (&x)[W],
                                                const Args& A) {
-    put<MW>(base, idx, red(x[0], A.p));
+    const uint32_t v = red(x[0], A.p);
+#if NTT_DEBUG_CHECKS
+    if (v >= A.p) ntt_dbg_flag(A.dbg, NTT_DBG_OUTPUT);
+#endif
+    put<MW>(base, idx, v);
   }
   __device__ static __forceinline__ void tload(Tw& t, const uint32_t* __restrict__ tab, size_t idx) {
     const uint2 v = reinterpret_cast<const uint2*>(tab)[idx];

@@ -106,6 +106,9 @@ struct PassArgs {
                              // [32 (1 + m)], ready at [32 (1 + m) + 1] (one 128-B line per slab)
   const uint32_t* ipn_order; // slab (middle-digit value) of the i-th slab in ticket order (pairs adjacent)
   uint32_t ipn_strips;       // workgroups per slab (R_1 / T)
+  // debug builds (NTT_DEBUG_CHECKS): element extents of src / dst from this transform's first element
+  // (~0: not checked, e.g. four-step maps into the caller's exchange blocks)
+  size_t dbg_src_n, dbg_dst_n;
 };
 enum : uint32_t { FS_MAP_IN = 1u, FS_MAP_OUT = 2u, FS_IL = 4u, FS_MAP_EPI = 8u };
 

@@ -59,7 +59,7 @@ struct Sched {
   static constexpr int logsig(int s) { return logN(s) - qb(s); }  // log2 sigma_s
 };
 template <class E>
-constexpr int ept_log() { return E::EPT == 8 ? 3 : (E::EPT == 4 ? 2 : 1); }
+constexpr int ept_log() { return E::EPT >= 8 ? 3 : (E::EPT == 4 ? 2 : 1); }  // register DFTs of <= 8 points
 
 // natural index of in-workgroup position pi after all sub-stages (digit reversal)
 template <int LOGR, int QB>
@@ -420,6 +420,16 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
     if (single_il) pos = (pos << A.il) + bq;
     return (A.fs & FS_MAP_EPI) ? A.mepi(pos, 0) : pos;
   };
+  // debug builds: an index outside its buffer is recorded and redirected to element 0
+  auto ck = [&](size_t i, [[maybe_unused]] size_t lim) -> size_t {
+#if NTT_DEBUG_CHECKS
+    if (i >= lim) {
+      ntt_dbg_flag(A.F.dbg, NTT_DBG_BOUNDS);
+      return 0;
+    }
+#endif
+    return i;
+  };
 
   // ------------------------------------------------------------------ workgroup geometry
   size_t colbase = 0;  // column pass: first element of this WG's column group
@@ -503,7 +513,14 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
         } else {
           pos = pi;
         }
-        E::template load<SW>(x[j * Q + d], src, NTT_NOMEM(IN_USER ? in_pos(pos) : pos));
+        E::template load<SW>(x[j * Q + d], src, ck(NTT_NOMEM(IN_USER ? in_pos(pos) : pos), A.dbg_src_n));
+#if NTT_DEBUG_CHECKS
+        // the caller's elements must be canonical (the reference's BAD LIMB trap); a column pass reads
+        // them only when A.src_user (one SRC_USER instance also serves later passes when the scratch
+        // and caller layouts agree)
+        if (KIND == KIND_SINGLE || (KIND == KIND_COLUMN && A.src_user))
+          if (!E::dbg_canonical(x[j * Q + d], A.F)) ntt_dbg_flag(A.F.dbg, NTT_DBG_INPUT);
+#endif
         if constexpr ((KIND == KIND_STOCKHAM || KIND == KIND_DIT) && FULLTW) {
           // bellperson's input twiddle (GZKP-NTT.cu:348-354): element pi of group k = index mod p is
           // multiplied by w_n^((n >> lgp >> deg) k pi), from a [k / T][pi][k mod T] table (p >= T).
@@ -575,12 +592,12 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
         if constexpr (KIND == KIND_DIT) {
           // in place (GZKP-NTT.cu:157-158): output k of column c back to c + s k of its block
           pos = colbase + c + ((size_t)kn << log_s);
-          E::template store<E::IN * Q, FAST, DW>(dst, NTT_NOMEM(pos), v, A.F);
+          E::template store<E::IN * Q, FAST, DW>(dst, ck(NTT_NOMEM(pos), A.dbg_dst_n), v, A.F);
         } else if constexpr (KIND == KIND_STOCKHAM) {
           // autosort store (GZKP-NTT.cu:378-384): y[((index - k) << deg) + k + kn p], k = index mod p
           const uint32_t idx = col0 + c, kk = idx & ((1u << A.lgp) - 1);
           pos = ((size_t)(idx - kk) << LOGR) + kk + ((size_t)kn << A.lgp);
-          E::template store<E::IN * Q, FAST, DW>(dst, NTT_NOMEM(pos), v, A.F);
+          E::template store<E::IN * Q, FAST, DW>(dst, ck(NTT_NOMEM(pos), A.dbg_dst_n), v, A.F);
         } else if constexpr (KIND == KIND_COLUMN) {
           if constexpr (FULLTW) {
             // outer twiddle w_{N_i}^{col * kn} R_e from the per-pass table (HBM element format,
@@ -612,7 +629,7 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
             E::mulv(v, tl.w, A.F);
           }
           pos = colbase + c + ((size_t)kn << log_s);
-          E::template store_lazy<E::MUL_OUT, FAST, DW, WT>(dst, NTT_NOMEM(pos), v, A.F);  // scratch: < 2p, read by the next pass
+          E::template store_lazy<E::MUL_OUT, FAST, DW, WT>(dst, ck(NTT_NOMEM(pos), A.dbg_dst_n), v, A.F);  // scratch: < 2p, read by the next pass
         } else if constexpr (KIND == KIND_FINAL) {
           if (fs_il) {
             const uint32_t k1 = k10 + (c >> tb_log), b = b0 + (c & ((1u << tb_log) - 1));
@@ -626,9 +643,9 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
             uint32_t tw[E::W];
             E::template load<E::SCRW>(tw, A.tw_epi, epi_idx(pos));
             E::mulv(v, tw, A.F);
-            E::template store<E::MUL_OUT, FAST, DW>(dst, NTT_NOMEM(out_pos(pos)), v, A.F);
+            E::template store<E::MUL_OUT, FAST, DW>(dst, ck(NTT_NOMEM(out_pos(pos)), A.dbg_dst_n), v, A.F);
           } else {
-            E::template store<E::IN * Q, FAST, DW>(dst, NTT_NOMEM(out_pos(pos)), v, A.F);
+            E::template store<E::IN * Q, FAST, DW>(dst, ck(NTT_NOMEM(out_pos(pos)), A.dbg_dst_n), v, A.F);
           }
         } else {
           pos = kn;
@@ -637,12 +654,12 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
             uint32_t tw[E::W];
             E::template load<E::SCRW>(tw, A.tw_epi, epi_idx(pos));
             E::mulv(v, tw, A.F);
-            E::template store<E::MUL_OUT, FAST>(dst, out_pos(pos), v, A.F);
+            E::template store<E::MUL_OUT, FAST>(dst, ck(out_pos(pos), A.dbg_dst_n), v, A.F);
           } else if (A.flags & 1u) {
             E::mul(v, A.F.ninv, A.F);
-            E::template store<E::MUL_OUT, FAST>(dst, out_pos(pos), v, A.F);
+            E::template store<E::MUL_OUT, FAST>(dst, ck(out_pos(pos), A.dbg_dst_n), v, A.F);
           } else {
-            E::template store<E::IN * Q, FAST>(dst, out_pos(pos), v, A.F);
+            E::template store<E::IN * Q, FAST>(dst, ck(out_pos(pos), A.dbg_dst_n), v, A.F);
           }
         }
       });

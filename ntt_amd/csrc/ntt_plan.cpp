@@ -414,6 +414,7 @@ struct PlanImpl final : PlanBase {
     if (d_sync) hipFree(d_sync);
     if (d_ipn) hipFree(d_ipn);
     if (d_pw) hipFree(d_pw);
+    if (d_dbg) hipFree(d_dbg);
     for (auto& row : ev)
       for (auto& e : row)
         if (e) hipEventDestroy(e);
@@ -589,6 +590,11 @@ struct PlanImpl final : PlanBase {
     if (hipMalloc(&d_tab, host.size() * 4) != hipSuccess ||
         hipMemcpy(d_tab, host.data(), host.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
       rc = NTT_ERR_HIP;
+#if NTT_DEBUG_CHECKS
+    // debug builds: the status word every kernel of this plan records check failures in
+    if (rc == NTT_OK && (hipMalloc(&d_dbg, 4) != hipSuccess || hipMemset(d_dbg, 0, 4) != hipSuccess)) rc = NTT_ERR_HIP;
+    Ff.dbg = Fi.dbg = d_dbg;
+#endif
     if (rc == NTT_OK && npass >= 2 && !twiddle_only && !(flags & NTT_PLAN_IN_PLACE)) rc = ensure_scratch(1);
     if (rc == NTT_OK && npass >= 2 && !twiddle_only) rc = build_full_tables();
     // NTT_PLAN_GZKP runs on the same per-pass tables: Stockham pass i's w_n^((k pi) << (log_n - lgp_i - r_i))
@@ -928,6 +934,13 @@ struct PlanImpl final : PlanBase {
     return NTT_OK;
   }
 
+  // debug builds: element extents of a pass's src / dst from the transform's first element (n per
+  // transform, n 2^il in Mode I); the four-step maps into the caller's exchange blocks stay unchecked
+  void set_extents(PassArgs<E>& A, const FsIO* io, uint32_t il) const {
+    const size_t ext = (size_t)n << il;
+    A.dbg_src_n = (io && (A.fs & FS_MAP_IN)) ? ~(size_t)0 : ext;
+    A.dbg_dst_n = (io && (A.fs & FS_MAP_OUT)) ? ~(size_t)0 : ext;
+  }
   PassArgs<E> base_args(bool inverse) const {
     PassArgs<E> A;
     memset(&A, 0, sizeof(A));
@@ -935,6 +948,7 @@ struct PlanImpl final : PlanBase {
     A.log_n = log_n;
     A.lo_bits = lo_bits;
     A.batch_stride = (size_t)n * MEMW;
+    A.dbg_src_n = A.dbg_dst_n = ~(size_t)0;  // debug builds: unchecked unless run_io knows the extents
     return A;
   }
 
@@ -989,6 +1003,7 @@ struct PlanImpl final : PlanBase {
       A.flags = inverse ? 1u : 0u;
       set_fs(A, FS_MAP_IN | FS_MAP_OUT);
       if (io) A.tw_epi = static_cast<const uint32_t*>(io->tw_epi);
+      set_extents(A, io, il);
       e = launch_pass<E>(KIND_SINGLE, (int)r[0], in, out, A, 1, il ? (1u << il) : batch, st);
       mark(st);
     } else {
@@ -1055,6 +1070,7 @@ struct PlanImpl final : PlanBase {
       set_fs(A, FS_MAP_OUT);
       if (io) A.tw_epi = static_cast<const uint32_t*>(io->tw_epi);
       if (inplace) A.flags |= 2u;
+      for (unsigned i = 0; i < npass; ++i) set_extents(PA[i], io, il);
       // XCD-grouped tile order (k_pass flag bit 2) for the column passes after the first whose runs are
       // shorter than a 128-B line (the 8-B path's 4-B scratch at radix 512: 64-B runs), so that the
       // two tiles sharing each line meet on one XCD's L2.  NTT_XCD_ORDER=0 off, =1 on every pass.
@@ -1182,8 +1198,15 @@ struct PlanImpl final : PlanBase {
       if (w && hipMemset(d + 2, 0, 4) != hipSuccess) return NTT_ERR_HIP;
       *bad |= w;
     }
+    if (d_dbg) {  // debug builds: NTT_DBG_* bits (engines.hpp)
+      uint32_t w = 0;
+      if (hipMemcpy(&w, d_dbg, 4, hipMemcpyDeviceToHost) != hipSuccess) return NTT_ERR_HIP;
+      if (w && hipMemset(d_dbg, 0, 4) != hipSuccess) return NTT_ERR_HIP;
+      *bad |= w;
+    }
     return NTT_OK;
   }
+  uint32_t* d_dbg = nullptr;  // debug builds (NTT_DEBUG_CHECKS): the kernels' check-failure bits
 
   // ---- in-place final pass with the fused digit reversal (NTT_PLAN_IN_PLACE, k_final_ipn)
   uint32_t* d_ipn = nullptr;  // 32 (1 + slabs) sync words, then the slab order table

@@ -148,7 +148,9 @@ class NTTPlan:
         return t
 
     def device_status(self) -> int:
-        """Watchdog word of the single-launch schedule (non-zero: a tile gave up waiting); clears it."""
+        """ntt_plan_device_status: bit 0 = a watchdog gave up (single launch / fused in-place digit
+        reversal); with the checked build (libntt_debug.so) 0x100 bounds, 0x200 non-canonical input,
+        0x400 lazy bound, 0x800 non-canonical output.  Blocking; clears the word."""
         v = C.c_uint()
         _L.check(self._lib.ntt_plan_device_status(self._h, C.byref(v)), "ntt_plan_device_status")
         return v.value

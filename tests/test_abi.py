@@ -40,6 +40,16 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
 
 
+def test_checked_build_exports_the_same_abi():
+    """ntt_amd/libntt_debug.so (NTT_DEBUG_CHECKS) is a drop-in for libntt.so: every declared symbol."""
+    from ntt_amd import build as B
+    if not os.path.exists(B.DEBUG_LIB):
+        pytest.skip("libntt_debug.so not built (python -m ntt_amd.build --debug)")
+    so = C.CDLL(B.DEBUG_LIB)
+    missing = [n for n in declared_functions() if not hasattr(so, n)]
+    assert not missing, missing
+
+
 def test_python_prototypes_cover_header():
     from ntt_amd import lib as L
     missing = [n for n in declared_functions() if n not in L.PROTOTYPES]

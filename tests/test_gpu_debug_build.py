@@ -1,0 +1,91 @@
+"""The checked build (ntt_amd/libntt_debug.so, NTT_DEBUG_CHECKS: in-kernel index bounds, canonical
+inputs and outputs, lazy bounds; VERDICT r02 missing item 4).  Run in a child process that loads it
+through NTT_LIB_PATH:
+
+* correct calls on every engine and schedule report a clean status and give the oracle's results,
+  so no check fires on legal data (the lazy bounds of DESIGN.md §4 hold at the checks);
+* a non-canonical input element (== p) is reported (0x200), once: reading the status clears it;
+* the edge vectors of test_gpu_edges (every lazy bound at its maximum) raise no check.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEBUG_LIB = os.path.join(ROOT, "ntt_amd", "libntt_debug.so")
+
+CHILD = r'''
+import sys
+sys.path.insert(0, ROOT)
+import numpy as np, torch
+from ntt_amd import lib as L
+from ntt_amd.ntt import NTTPlan
+from oracle import ntt_ref as R
+from oracle import oracle_c as OC
+lib = L.load()
+assert L.LIB_PATH.endswith("libntt_debug.so"), L.LIB_PATH
+
+def host(t, limbs):
+    return t.cpu().numpy().view(np.uint64).reshape(-1, limbs).copy()
+
+# clean runs: oracle parity at 2^14 and round trips, every engine; in place; polymul; batch
+for fid, lg, limbs, flags in ((1, 14, 4, {}), (2, 14, 6, {}), (0, 14, 1, {}), (1, 20, 4, {}), (2, 18, 4, {}),
+                              (0, 22, 1, {}), (1, 20, 4, {"in_place": True}), (0, 20, 1, {"in_place": True}),
+                              (1, 20, 4, {"single_launch": True})):
+    pl = NTTPlan(fid, lg, limbs, **flags)
+    t = pl.fill(pl.empty(), "random", seed=3)
+    x = t.clone()
+    pl.forward(t)
+    if lg <= 14:
+        p, g = R.FIELDS[fid]
+        exp = OC.ntt_mp(host(x, limbs), p, g)
+        assert np.array_equal(host(t, limbs), exp), (fid, lg, limbs)
+    pl.inverse(t)
+    assert torch.equal(t, x), (fid, lg, limbs, flags)
+    st = pl.device_status()
+    assert st == 0, (fid, lg, limbs, flags, hex(st))
+pl = NTTPlan(1, 16, 4)
+a, b, c = pl.fill(pl.empty(), "random", seed=5), pl.fill(pl.empty(), "random", seed=6), pl.empty()
+pl.polymul(a, b, c)
+assert pl.device_status() == 0
+print("CLEAN-OK")
+
+# a non-canonical input: element 5 := p
+for fid, limbs in ((1, 4), (0, 1)):
+    pl = NTTPlan(fid, 16, limbs)
+    t = pl.fill(pl.empty(), "random", seed=7)
+    p = R.FIELDS[fid][0]
+    bad = torch.from_numpy(OC.ints_to_limbs([p], limbs).view(np.int64).reshape(-1)).to(t.device)
+    if limbs == 1:
+        t[5] = bad[0]
+    else:
+        t[5] = bad
+    pl.forward(t)
+    st = pl.device_status()
+    assert st & 0x200, (fid, hex(st))
+    assert pl.device_status() == 0  # cleared
+print("INPUT-OK")
+'''
+
+
+@pytest.mark.skipif(not os.path.exists(DEBUG_LIB), reason="libntt_debug.so not built (python -m ntt_amd.build --debug)")
+def test_checked_build_clean_runs_and_noncanonical_input():
+    env = dict(os.environ, NTT_LIB_PATH=DEBUG_LIB)
+    r = subprocess.run([sys.executable, "-c", f"ROOT = {ROOT!r}\n" + CHILD], env=env, capture_output=True, text=True,
+                       timeout=280)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert "CLEAN-OK" in r.stdout and "INPUT-OK" in r.stdout
+
+
+@pytest.mark.skipif(not os.path.exists(DEBUG_LIB), reason="libntt_debug.so not built (python -m ntt_amd.build --debug)")
+def test_checked_build_on_the_edge_vectors():
+    """The adversarial inputs of test_gpu_edges (constants p - 1, deltas, near-p patterns: every lazy
+    bound at its maximum) through the checked build: bit-exact, and no in-kernel check fires."""
+    env = dict(os.environ, NTT_LIB_PATH=DEBUG_LIB)
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider",
+                        os.path.join(ROOT, "tests", "test_gpu_edges.py")], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=280)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-2000:])

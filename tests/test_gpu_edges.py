@@ -45,6 +45,9 @@ def _values(arr):
 def _run(pl, host, inverse=False):
     t = torch.from_numpy(np.ascontiguousarray(host).view(np.int64)).to("cuda:0").reshape(host.shape)
     (pl.inverse if inverse else pl.forward)(t)
+    # the checked build (libntt_debug.so, tests/test_gpu_debug_build.py) checks every lazy bound in the
+    # kernels: these inputs drive them to their maxima, so no check may fire; the product build reports 0
+    assert pl.device_status() == 0, hex(pl.device_status())
     return t.cpu().numpy().view(np.uint64).reshape(host.shape)
 
 
