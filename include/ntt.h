@@ -310,9 +310,14 @@ int ntt_polymul_multi(ntt_mplan* plan, void* const* d_a, void* const* d_b, void*
 /* each device's row-layout share of the global synthetic vector (kinds as ntt_fill) */
 int ntt_mplan_fill(ntt_mplan* plan, void* const* d_data, int kind, uint64_t seed, void* const* hip_streams);
 int ntt_mplan_info(const ntt_mplan* plan, uint64_t* local_n, unsigned* log_n1, unsigned* log_n2);
-/* Row pieces of the pipelined exchange (1..16, <= r): piece i's all-to-all (grouped ncclSend /
- * ncclRecv on a per-device communication stream) overlaps the row transforms of piece i + 1.
- * Default: pieces of >= 2^22 elements (1 for 2^24 over 8 GPUs, 8 for 2^28). */
+/* Pieces of the pipelined exchange on both sides (powers of two, <= 16, row_pieces <= r, col_pieces
+ * <= c; the ntt_rplan_*_piece layouts): row piece i's exchange (grouped ncclSend / ncclRecv on a
+ * per-device communication stream) overlaps the row transforms of piece i + 1, the last row piece
+ * goes out per column piece and each column piece's transforms start when it has arrived (the
+ * inverse mirrors it).  Default: row pieces of >= 2^22 elements, column pieces of >= 2^21, at most 4
+ * (2^24 over 2 GPUs: 2 x 4; over 8: 1 x 1; 2^28 over 8: 8 x 4). */
+int ntt_mplan_set_pieces2(ntt_mplan* plan, unsigned row_pieces, unsigned col_pieces);
+/* Row pieces only (1..16, <= r; rounded down to a power of two), one column piece. */
 int ntt_mplan_set_pieces(ntt_mplan* plan, unsigned pieces);
 int ntt_mplan_destroy(ntt_mplan* plan);
 

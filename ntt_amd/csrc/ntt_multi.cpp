@@ -12,11 +12,13 @@
 // inverse mirrors it (column layout in, row layout out).  All work is asynchronous on the callers'
 // per-device streams.  The reference has no multi-GPU code.
 //
-// Pipelined exchange (as DistNTT, ntt_amd/distributed.py): the row steps run in row pieces
-// (ntt_rplan_*_rows_range); rows [a0, a0 + m) of every peer chunk are one contiguous run, so piece i
-// is exchanged (grouped ncclSend / ncclRecv on a per-device communication stream, ordered by events)
-// while the row transforms of piece i + 1 run, and the inverse transforms piece i as soon as it has
-// arrived.  Pieces keep >= 2^22 elements each (full launches); ntt_mplan_set_pieces overrides.
+// Pipelined exchange on both sides (the schedule of FourStep, ntt_amd/distributed.py): P_r row pieces
+// x P_c column pieces (ntt_rplan_*_piece; every exchange unit is one contiguous run of a peer block).
+// Forward: row piece i is exchanged (grouped ncclSend / ncclRecv on a per-device communication
+// stream, ordered by events) while the row transforms of piece i + 1 run; the last row piece goes out
+// column piece by column piece, and the column transforms of piece k start when its unit has arrived.
+// The inverse mirrors it.  Row pieces keep >= 2^22 elements, column pieces >= 2^21 (at most 4);
+// ntt_mplan_set_pieces / ntt_mplan_set_pieces2 override.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -91,7 +93,8 @@ struct ntt_mplan {
   std::vector<hipStream_t> cstream;   // per-device communication stream (pipelined exchange)
   std::vector<hipEvent_t> ev_ready;   // per device: compute -> communication ordering
   std::vector<hipEvent_t> ev_done;    // per device and piece: arrival of piece i (kMaxPieces each)
-  unsigned pieces = 1;
+  unsigned pieces = 1;      // row pieces P_r (power of two)
+  unsigned col_pieces = 1;  // column pieces P_c (power of two)
   // set when an exchange failed: the communicators were aborted (a peer may have posted its part of
   // the collective) and every later call returns NTT_ERR_RCCL
   bool broken = false;
@@ -186,13 +189,15 @@ size_t chunk_words(const ntt_mplan* m) {  // per-peer chunk of one vector: r * c
   return (1ull << (m->log_r + m->log_c)) * (m->elem_bytes / 8);
 }
 
-// Rows [row0, row0 + nrows) of every peer chunk of nv vectors (buffers [G][nv][chunk]), as grouped
-// ncclSend / ncclRecv on the communication streams.
-int exchange_rows(ntt_mplan* m, const std::vector<void*>& send, const std::vector<void*>& recv, int nv,
-                  size_t row0, size_t nrows) {
+// Runs of every peer block (blocks of peer_elems elements; runs (offset, length) in elements) as
+// grouped ncclSend / ncclRecv on the communication streams.
+struct Run {
+  size_t off, len;
+};
+int exchange_runs(ntt_mplan* m, const std::vector<void*>& send, const std::vector<void*>& recv, size_t peer_elems,
+                  const std::vector<Run>& runs) {
   const Rccl& R = rccl();
-  const size_t cw = chunk_words(m), rw = cw >> m->log_r;  // words per chunk, per chunk row
-  const size_t off0 = row0 * rw, words = nrows * rw, piece = kMaxPeerBytes / 8;
+  const size_t E = m->elem_bytes / 8, piece = kMaxPeerBytes / 8;
   if (R.GroupStart() != ncclSuccess) return NTT_ERR_RCCL;
   ncclResult_t st = ncclSuccess;
   for (int g = 0; g < m->ngpus && st == ncclSuccess; ++g) {
@@ -200,8 +205,8 @@ int exchange_rows(ntt_mplan* m, const std::vector<void*>& send, const std::vecto
     auto* sb = static_cast<uint64_t*>(send[g]);
     auto* rb = static_cast<uint64_t*>(recv[g]);
     for (int h = 0; h < m->ngpus && st == ncclSuccess; ++h)
-      for (int k = 0; k < nv && st == ncclSuccess; ++k) {
-        const size_t base = (size_t)(h * nv + k) * cw + off0;
+      for (const Run& u : runs) {
+        const size_t base = (h * peer_elems + u.off) * E, words = u.len * E;
         for (size_t off = 0; off < words && st == ncclSuccess; off += piece) {
           const size_t cnt = words - off < piece ? words - off : piece;
           st = R.Send(sb + base + off, cnt, ncclUint64, h, m->comm[g], m->cstream[g]);
@@ -239,12 +244,6 @@ int record_piece(ntt_mplan* m, unsigned i) {
     if (hipEventRecord(m->done(g, i), m->cstream[g]) != hipSuccess) return NTT_ERR_HIP;
   }
   return NTT_OK;
-}
-
-void piece_range(const ntt_mplan* m, unsigned i, size_t& row0, size_t& nrows) {
-  const size_t r = 1ull << m->log_r, step = (r + m->pieces - 1) / m->pieces;
-  row0 = i * step;
-  nrows = row0 >= r ? 0 : (r - row0 < step ? r - row0 : step);
 }
 
 // After a failed step the other devices may still hold queued work that reads or writes the
@@ -286,33 +285,45 @@ int ensure_pair_buffers(ntt_mplan* m) {
 int forward_vectors(ntt_mplan* m, void* const* const* v, int nv, void* const* streams) {
   const std::vector<void*>& sb = nv == 1 ? m->send : m->send2;
   const std::vector<void*>& rb = nv == 1 ? m->recv : m->recv2;
-  if (m->pieces == 1) {
+  if (m->pieces == 1 && m->col_pieces == 1) {
     for (int g = 0; g < m->ngpus; ++g)
       for (int k = 0; k < nv; ++k)
         if (int rc = ntt_rplan_forward_rows(m->rp[g], v[k][g], sb[g], (unsigned)nv, (unsigned)k,
                                             m->stream(streams, g)))
           return rc;
     if (int rc = exchange(m, sb, rb, nv * chunk_words(m), streams)) return rc;
-  } else {  // piece i's exchange overlaps the row transforms of piece i + 1
-    for (unsigned i = 0; i < m->pieces; ++i) {
-      size_t a0, ra;
-      piece_range(m, i, a0, ra);
-      if (ra == 0) break;
+  } else {
+    // row piece i's exchange overlaps the row transforms of piece i + 1; the last row piece goes out
+    // per column piece, whose column transforms start as soon as that unit has arrived
+    const unsigned P = m->pieces, Q = m->col_pieces;
+    const size_t c = 1ull << m->log_c, ra = (1ull << m->log_r) / P, cm = c / Q, peer = nv * m->local_n();
+    for (unsigned i = 0; i < P; ++i) {
       for (int g = 0; g < m->ngpus; ++g)
         for (int k = 0; k < nv; ++k)
-          if (int rc = ntt_rplan_forward_rows_range(m->rp[g], v[k][g], sb[g], (unsigned)nv, (unsigned)k, a0, ra,
+          if (int rc = ntt_rplan_forward_rows_piece(m->rp[g], v[k][g], sb[g], (unsigned)nv, (unsigned)k, i, P, Q,
                                                     m->stream(streams, g)))
             return rc;
       if (int rc = order_comm_after_compute(m, streams)) return rc;
-      if (int rc = exchange_rows(m, sb, rb, nv, a0, ra)) return rc;
-      if (int rc = record_piece(m, i)) return rc;
+      if (i + 1 < P) {
+        if (int rc = exchange_runs(m, sb, rb, peer, {Run{i * nv * ra * c, nv * ra * c}})) return rc;
+        continue;
+      }
+      for (unsigned q = 0; q < Q; ++q) {
+        std::vector<Run> units;
+        for (int k = 0; k < nv; ++k) units.push_back(Run{(i * nv + k) * ra * c + q * ra * cm, ra * cm});
+        if (int rc = exchange_runs(m, sb, rb, peer, units)) return rc;
+        if (int rc = record_piece(m, q)) return rc;
+      }
     }
-    for (unsigned i = 0; i < m->pieces; ++i) {  // only the pieces exchanged above (a short last one ends it)
-      size_t a0, ra;
-      piece_range(m, i, a0, ra);
-      if (ra == 0) break;
-      if (int rc = order_compute_after_piece(m, streams, i)) return rc;
+    for (unsigned q = 0; q < Q; ++q) {  // event q: unit q of the last row piece and everything before it
+      if (int rc = order_compute_after_piece(m, streams, q)) return rc;
+      for (int g = 0; g < m->ngpus; ++g)
+        for (int k = 0; k < nv; ++k)
+          if (int rc = ntt_rplan_forward_cols_piece(m->rp[g], rb[g], v[k][g], (unsigned)nv, (unsigned)k, q, P, Q,
+                                                    m->stream(streams, g)))
+            return rc;
     }
+    return NTT_OK;
   }
   for (int g = 0; g < m->ngpus; ++g)
     for (int k = 0; k < nv; ++k)
@@ -324,31 +335,38 @@ int forward_vectors(ntt_mplan* m, void* const* const* v, int nv, void* const* st
 // Inverse from column layout to row layout; with b (polymul) the first column pass starts from the
 // pointwise product a * b and the result lands in `out`.
 int inverse_vector(ntt_mplan* m, void* const* a, void* const* b, void* const* out, void* const* streams) {
-  for (int g = 0; g < m->ngpus; ++g)
-    if (int rc = ntt_rplan_inverse_cols(m->rp[g], a[g], b ? b[g] : nullptr, m->send[g], m->stream(streams, g)))
-      return rc;
-  if (m->pieces == 1) {
+  const unsigned P = m->pieces, Q = m->col_pieces;
+  if (P == 1 && Q == 1) {
+    for (int g = 0; g < m->ngpus; ++g)
+      if (int rc = ntt_rplan_inverse_cols(m->rp[g], a[g], b ? b[g] : nullptr, m->send[g], m->stream(streams, g)))
+        return rc;
     if (int rc = exchange(m, m->send, m->recv, chunk_words(m), streams)) return rc;
     for (int g = 0; g < m->ngpus; ++g)
       if (int rc = ntt_rplan_inverse_rows(m->rp[g], m->recv[g], out[g], m->stream(streams, g))) return rc;
     return NTT_OK;
   }
-  // every piece's exchange is queued on the comm streams; piece i's row transforms wait only for it
-  if (int rc = order_comm_after_compute(m, streams)) return rc;
-  for (unsigned i = 0; i < m->pieces; ++i) {
-    size_t a0, ra;
-    piece_range(m, i, a0, ra);
-    if (ra == 0) break;
-    if (int rc = exchange_rows(m, m->send, m->recv, 1, a0, ra)) return rc;
-    if (int rc = record_piece(m, i)) return rc;
+  // column piece q's exchange overlaps the column transforms of piece q + 1; the last column piece
+  // goes out per row piece, whose inverse row transforms start as soon as that unit has arrived
+  const size_t r = 1ull << m->log_r, ra = r / P, cm = (1ull << m->log_c) / Q, peer = m->local_n();
+  for (unsigned q = 0; q < Q; ++q) {
+    for (int g = 0; g < m->ngpus; ++g)
+      if (int rc = ntt_rplan_inverse_cols_piece(m->rp[g], a[g], b ? b[g] : nullptr, m->send[g], q, P, Q,
+                                                m->stream(streams, g)))
+        return rc;
+    if (int rc = order_comm_after_compute(m, streams)) return rc;
+    if (q + 1 < Q) {
+      if (int rc = exchange_runs(m, m->send, m->recv, peer, {Run{q * r * cm, r * cm}})) return rc;
+      continue;
+    }
+    for (unsigned i = 0; i < P; ++i) {
+      if (int rc = exchange_runs(m, m->send, m->recv, peer, {Run{q * r * cm + i * ra * cm, ra * cm}})) return rc;
+      if (int rc = record_piece(m, i)) return rc;
+    }
   }
-  for (unsigned i = 0; i < m->pieces; ++i) {
-    size_t a0, ra;
-    piece_range(m, i, a0, ra);
-    if (ra == 0) break;
+  for (unsigned i = 0; i < P; ++i) {
     if (int rc = order_compute_after_piece(m, streams, i)) return rc;
     for (int g = 0; g < m->ngpus; ++g)
-      if (int rc = ntt_rplan_inverse_rows_range(m->rp[g], m->recv[g], out[g], a0, ra, m->stream(streams, g)))
+      if (int rc = ntt_rplan_inverse_rows_piece(m->rp[g], m->recv[g], out[g], i, P, Q, m->stream(streams, g)))
         return rc;
   }
   return NTT_OK;
@@ -403,10 +421,12 @@ int ntt_mplan_create(ntt_mplan** out, int field_id, unsigned log_n, unsigned lim
         if (hipEventCreateWithFlags(&m->ev_done[g * ntt_mplan::kMaxPieces + i], hipEventDisableTiming) != hipSuccess)
           rc = NTT_ERR_HIP;
     }
-    // pieces of >= 2^22 elements (DistNTT.auto_pieces)
+    // row pieces of >= 2^22 elements, column pieces of >= 2^21 (at most 4): DistNTT.auto_pieces
     const size_t local = m->local_n();
     while (m->pieces < 8 && (local >> 1) / m->pieces >= (size_t(1) << 22)) m->pieces *= 2;
+    while (m->col_pieces < 4 && (local >> 1) / m->col_pieces >= (size_t(1) << 21)) m->col_pieces *= 2;
     if (m->pieces > (1u << m->log_r)) m->pieces = 1u << m->log_r;
+    if (m->col_pieces > (1u << m->log_c)) m->col_pieces = 1u << m->log_c;
   }
   if (rc != NTT_OK) {
     delete m;
@@ -456,10 +476,22 @@ int ntt_mplan_fill(ntt_mplan* m, void* const* d_data, int kind, uint64_t seed, v
   return NTT_OK;
 }
 
-int ntt_mplan_set_pieces(ntt_mplan* m, unsigned pieces) {
-  if (!m || pieces < 1 || pieces > ntt_mplan::kMaxPieces || pieces > (1u << m->log_r)) return NTT_ERR_ARG;
-  m->pieces = pieces;
+int ntt_mplan_set_pieces2(ntt_mplan* m, unsigned row_pieces, unsigned col_pieces) {
+  if (!m || row_pieces < 1 || col_pieces < 1 || (row_pieces & (row_pieces - 1)) || (col_pieces & (col_pieces - 1)) ||
+      row_pieces > ntt_mplan::kMaxPieces || col_pieces > ntt_mplan::kMaxPieces || row_pieces > (1u << m->log_r) ||
+      col_pieces > (1u << m->log_c))
+    return NTT_ERR_ARG;
+  m->pieces = row_pieces;
+  m->col_pieces = col_pieces;
   return NTT_OK;
+}
+
+int ntt_mplan_set_pieces(ntt_mplan* m, unsigned pieces) {
+  // row pieces only (the round-2 entry point); a count that is not a power of two rounds down
+  if (!m || pieces < 1 || pieces > ntt_mplan::kMaxPieces || pieces > (1u << m->log_r)) return NTT_ERR_ARG;
+  unsigned p = 1;
+  while (p * 2 <= pieces) p *= 2;
+  return ntt_mplan_set_pieces2(m, p, 1);
 }
 
 int ntt_mplan_info(const ntt_mplan* m, uint64_t* local_n, unsigned* log_n1, unsigned* log_n2) {

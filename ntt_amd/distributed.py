@@ -559,8 +559,9 @@ class MultiPlan:
     """
 
     def __init__(self, field_id: int = 1, log_n: int = 24, limbs64: int = 4, devices: Optional[List[int]] = None,
-                 pieces: Optional[int] = None):
-        """pieces: row pieces of the pipelined exchange (None: the plan's default, >= 2^22 elements each)."""
+                 pieces: Optional[int] = None, col_pieces: Optional[int] = None):
+        """pieces / col_pieces: row / column pieces of the pipelined exchange (None, None: the plan's
+        default; pieces alone: row pieces only, ntt_mplan_set_pieces; both: ntt_mplan_set_pieces2)."""
         from . import lib as _L
         self._L = _L
         self.lib = _L.load()
@@ -575,7 +576,9 @@ class MultiPlan:
         self.lib.ntt_mplan_info(h, C.byref(local_n), C.byref(n1), C.byref(n2))
         self.local_n, self.log_n1, self.log_n2 = local_n.value, n1.value, n2.value
         self.layouts = [Layout(log_n, len(self.devices), g, self.log_n2) for g in range(len(self.devices))]
-        if pieces is not None:
+        if col_pieces is not None:
+            _L.check(self.lib.ntt_mplan_set_pieces2(h, int(pieces or 1), int(col_pieces)), "ntt_mplan_set_pieces2")
+        elif pieces is not None:
             _L.check(self.lib.ntt_mplan_set_pieces(h, int(pieces)), "ntt_mplan_set_pieces")
 
     def __del__(self):

@@ -62,6 +62,7 @@ PROTOTYPES = {
     "ntt_mplan_fill": (C.c_int, [_vp, C.POINTER(_vp), C.c_int, C.c_uint64, C.POINTER(_vp)]),
     "ntt_mplan_info": (C.c_int, [_vp, C.POINTER(C.c_uint64), C.POINTER(C.c_uint), C.POINTER(C.c_uint)]),
     "ntt_mplan_set_pieces": (C.c_int, [_vp, C.c_uint]),
+    "ntt_mplan_set_pieces2": (C.c_int, [_vp, C.c_uint, C.c_uint]),
     "ntt_mplan_destroy": (C.c_int, [_vp]),
     "ntt_count_noncanonical": (C.c_int, [_vp, _vp, C.c_uint64, C.POINTER(C.c_uint64), _vp]),
     "ntt_plan_device_status": (C.c_int, [_vp, C.POINTER(C.c_uint)]),

@@ -103,17 +103,21 @@ def test_dist_ntt_rccl_world1():
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("log_n,field_id,L,pieces", [(12, 1, 4, None), (17, 1, 4, None), (16, 2, 6, None),
-                                                      (14, 0, 1, None), (12, 1, 4, 4), (17, 1, 4, 3), (16, 2, 6, 16),
-                                                      (14, 0, 1, 2)])
-def test_mplan_single_process_rccl(log_n, field_id, L, pieces):
+@pytest.mark.parametrize("log_n,field_id,L,pieces,col_pieces",
+                         [(12, 1, 4, None, None), (17, 1, 4, None, None), (16, 2, 6, None, None),
+                          (14, 0, 1, None, None), (12, 1, 4, 4, None), (17, 1, 4, 3, None), (16, 2, 6, 16, None),
+                          (14, 0, 1, 2, None), (12, 1, 4, 1, 4), (16, 1, 4, 4, 8), (14, 0, 1, 2, 2),
+                          (16, 2, 6, 2, 4), (24, 1, 4, None, None)])
+def test_mplan_single_process_rccl(log_n, field_id, L, pieces, col_pieces):
     """ntt_mplan_* (one process, ncclCommInitAll over the visible devices, grouped all-to-all):
     the column-layout output equals the single-GPU transform; the inverse restores the rows.
-    pieces: the pipelined exchange (grouped ncclSend/ncclRecv of row pieces on the plan's
-    communication streams, uneven last piece included)."""
+    pieces / col_pieces: the pipelined exchange on both sides (grouped ncclSend/ncclRecv of the
+    exchange units on the plan's communication streams; 3 rounds down to 2; 2^24 on one device: the
+    default pieces)."""
     from ntt_amd.distributed import MultiPlan
     from ntt_amd.ntt import NTTPlan
-    mp = MultiPlan(field_id, log_n, L, devices=list(range(torch.cuda.device_count())), pieces=pieces)
+    mp = MultiPlan(field_id, log_n, L, devices=list(range(torch.cuda.device_count())), pieces=pieces,
+                   col_pieces=col_pieces)
     xs = mp.fill(mp.empty(), "random", seed=11)
     ref = NTTPlan(field_id, log_n, L)
     x = ref.fill(ref.empty(), "random", seed=11)

@@ -96,12 +96,16 @@ def test_c5_polymul_2pow24_eight_virtual_ranks():
         assert torch.equal(o, exp[_row_index(lay, o.device)]), lay.rank
 
 
-@pytest.mark.parametrize("log_n,pieces", [(16, None), (24, None), (16, 4), (24, 8)])
-def test_mplan_polymul_matches_single_gpu(log_n, pieces):
+@pytest.mark.parametrize("log_n,pieces,col_pieces", [(16, None, None), (24, None, None), (16, 4, None), (24, 8, None),
+                                                     (16, 4, 4), (24, 2, 4), (14, 2, 2)])
+def test_mplan_polymul_matches_single_gpu(log_n, pieces, col_pieces):
+    """col_pieces: the two-sided schedule (a and b in every unit of the forward; the product fused
+    into the inverse's column pieces, or gathered at 2^14 where the column transforms are one pass)."""
     from ntt_amd.distributed import MultiPlan
     fid, L = 1, 4
     exp = _single_gpu_product(fid, L, log_n, 5, 6)
-    mp = MultiPlan(fid, log_n, L, devices=list(range(torch.cuda.device_count())), pieces=pieces)
+    mp = MultiPlan(fid, log_n, L, devices=list(range(torch.cuda.device_count())), pieces=pieces,
+                   col_pieces=col_pieces)
     As = mp.fill(mp.empty(), "random", seed=5)
     Bs = mp.fill(mp.empty(), "random", seed=6)
     Outs = mp.empty()
