@@ -12,7 +12,8 @@
 #include "field29_asm9.hpp"
 
 // timing-only experiment builds (never the product): bit 0 drops the reductions, bit 1 the Shoup
-// products, bit 2 the Montgomery products, bit 3 the carry normalisations (tools/r03_ab.sh)
+// products, bit 2 the Montgomery products, bit 3 the carry normalisations, bit 4 folds the first
+// pass's n-entry outer-twiddle table reads into an L2-resident window (tools/r03_ab.sh)
 #ifndef NTT_AB_SKIP
 #define NTT_AB_SKIP 0
 #endif

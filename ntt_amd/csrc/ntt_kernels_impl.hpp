@@ -615,6 +615,9 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
               E::tload(tws, A.tw_full, NTT_NOMEM(ti));
               E::mul(v, tws, A.F);
             } else {
+#if NTT_AB_SKIP & 16  // timing-only (tools/r03_ab.sh): the table reads folded into an L2-resident window
+              ti &= (size_t(1) << 14) - 1;
+#endif
               E::template load<E::SCRW>(tw, A.tw_full, NTT_NOMEM(ti));
               E::mulv(v, tw, A.F);
             }

@@ -127,8 +127,8 @@ namespace {
 
 struct DeviceGuard {
   int cur = 0;
-  DeviceGuard() { hipGetDevice(&cur); }
-  ~DeviceGuard() { hipSetDevice(cur); }
+  DeviceGuard() { (void)hipGetDevice(&cur); }
+  ~DeviceGuard() { (void)hipSetDevice(cur); }
 };
 
 // RCCL moves at most 2^31 - 1 bytes per peer per collective (a 2 GiB per-peer chunk arrived half
@@ -161,13 +161,13 @@ int exchange(ntt_mplan* m, const std::vector<void*>& send, const std::vector<voi
   ncclResult_t st = ncclSuccess;
   if (words * 8 <= kMaxPeerBytes) {
     for (int g = 0; g < m->ngpus && st == ncclSuccess; ++g) {
-      hipSetDevice(m->dev[g]);
+      (void)hipSetDevice(m->dev[g]);  // inside the group: RCCL calls carry their communicator's device
       st = R.AllToAll(send[g], recv[g], words, ncclUint64, m->comm[g], m->stream(streams, g));
     }
   } else {
     const size_t piece = kMaxPeerBytes / 8;
     for (int g = 0; g < m->ngpus && st == ncclSuccess; ++g) {
-      hipSetDevice(m->dev[g]);
+      (void)hipSetDevice(m->dev[g]);  // inside the group: RCCL calls carry their communicator's device
       hipStream_t s = m->stream(streams, g);
       auto* sb = static_cast<uint64_t*>(send[g]);
       auto* rb = static_cast<uint64_t*>(recv[g]);
@@ -201,7 +201,7 @@ int exchange_runs(ntt_mplan* m, const std::vector<void*>& send, const std::vecto
   if (R.GroupStart() != ncclSuccess) return NTT_ERR_RCCL;
   ncclResult_t st = ncclSuccess;
   for (int g = 0; g < m->ngpus && st == ncclSuccess; ++g) {
-    hipSetDevice(m->dev[g]);
+    (void)hipSetDevice(m->dev[g]);  // inside the group: RCCL calls carry their communicator's device
     auto* sb = static_cast<uint64_t*>(send[g]);
     auto* rb = static_cast<uint64_t*>(recv[g]);
     for (int h = 0; h < m->ngpus && st == ncclSuccess; ++h)
@@ -221,7 +221,7 @@ int exchange_runs(ntt_mplan* m, const std::vector<void*>& send, const std::vecto
 // comm stream of every device waits for the work enqueued so far on its compute stream
 int order_comm_after_compute(ntt_mplan* m, void* const* streams) {
   for (int g = 0; g < m->ngpus; ++g) {
-    hipSetDevice(m->dev[g]);
+    if (hipSetDevice(m->dev[g]) != hipSuccess) return NTT_ERR_HIP;
     if (hipEventRecord(m->ev_ready[g], m->stream(streams, g)) != hipSuccess ||
         hipStreamWaitEvent(m->cstream[g], m->ev_ready[g], 0) != hipSuccess)
       return NTT_ERR_HIP;
@@ -232,7 +232,7 @@ int order_comm_after_compute(ntt_mplan* m, void* const* streams) {
 // compute stream of every device waits for piece i's arrival (recorded on its comm stream)
 int order_compute_after_piece(ntt_mplan* m, void* const* streams, unsigned i) {
   for (int g = 0; g < m->ngpus; ++g) {
-    hipSetDevice(m->dev[g]);
+    if (hipSetDevice(m->dev[g]) != hipSuccess) return NTT_ERR_HIP;
     if (hipStreamWaitEvent(m->stream(streams, g), m->done(g, i), 0) != hipSuccess) return NTT_ERR_HIP;
   }
   return NTT_OK;
@@ -240,7 +240,7 @@ int order_compute_after_piece(ntt_mplan* m, void* const* streams, unsigned i) {
 
 int record_piece(ntt_mplan* m, unsigned i) {
   for (int g = 0; g < m->ngpus; ++g) {
-    hipSetDevice(m->dev[g]);
+    if (hipSetDevice(m->dev[g]) != hipSuccess) return NTT_ERR_HIP;
     if (hipEventRecord(m->done(g, i), m->cstream[g]) != hipSuccess) return NTT_ERR_HIP;
   }
   return NTT_OK;

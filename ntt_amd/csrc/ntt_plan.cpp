@@ -122,7 +122,7 @@ struct PlanBase {
     mark(st);
   }
   void mark(hipStream_t st) {
-    if (profiling && ev_used < kEv) hipEventRecord(ev[slot][ev_used++], st);
+    if (profiling && ev_used < kEv) (void)hipEventRecord(ev[slot][ev_used++], st);
   }
 };
 
@@ -397,28 +397,28 @@ struct PlanImpl final : PlanBase {
 
   ~PlanImpl() override {
     int cur = 0;
-    hipGetDevice(&cur);
-    hipSetDevice(device);
-    if (d_tab) hipFree(d_tab);
-    if (d_scratch) hipFree(d_scratch);
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(device);
+    if (d_tab) (void)hipFree(d_tab);
+    if (d_scratch) (void)hipFree(d_scratch);
     for (auto* p : d_fulls)
-      if (p) hipFree(p);
-    if (d_full_sh) hipFree(d_full_sh);
-    if (d_full_pm) hipFree(d_full_pm);
-    if (d_stk_tab) hipFree(d_stk_tab);
+      if (p) (void)hipFree(p);
+    if (d_full_sh) (void)hipFree(d_full_sh);
+    if (d_full_pm) (void)hipFree(d_full_pm);
+    if (d_stk_tab) (void)hipFree(d_stk_tab);
     for (auto* p : d_stk_buf)
-      if (p) hipFree(p);
-    if (d_bad) hipFree(d_bad);
-    if (d_coset) hipFree(d_coset);
-    if (d_coset_full) hipFree(d_coset_full);
-    if (d_sync) hipFree(d_sync);
-    if (d_ipn) hipFree(d_ipn);
-    if (d_pw) hipFree(d_pw);
-    if (d_dbg) hipFree(d_dbg);
+      if (p) (void)hipFree(p);
+    if (d_bad) (void)hipFree(d_bad);
+    if (d_coset) (void)hipFree(d_coset);
+    if (d_coset_full) (void)hipFree(d_coset_full);
+    if (d_sync) (void)hipFree(d_sync);
+    if (d_ipn) (void)hipFree(d_ipn);
+    if (d_pw) (void)hipFree(d_pw);
+    if (d_dbg) (void)hipFree(d_dbg);
     for (auto& row : ev)
       for (auto& e : row)
-        if (e) hipEventDestroy(e);
-    hipSetDevice(cur);
+        if (e) (void)hipEventDestroy(e);
+    (void)hipSetDevice(cur);
   }
 
   // modulus / generator as NH 32-bit words
@@ -584,7 +584,7 @@ struct PlanImpl final : PlanBase {
     }
     pm2_ = pm2;
     int cur = 0;
-    hipGetDevice(&cur);
+    (void)hipGetDevice(&cur);
     if (hipSetDevice(device) != hipSuccess) return NTT_ERR_HIP;
     int rc = NTT_OK;
     if (hipMalloc(&d_tab, host.size() * 4) != hipSuccess ||
@@ -600,7 +600,7 @@ struct PlanImpl final : PlanBase {
     // NTT_PLAN_GZKP runs on the same per-pass tables: Stockham pass i's w_n^((k pi) << (log_n - lgp_i - r_i))
     // for k < 2^lgp_i is the GZKP DIT pass's w_N^(c d), N = 2^(lgp_i + r_i)
     if (rc == NTT_OK && (flags & (NTT_PLAN_STOCKHAM | NTT_PLAN_GZKP))) rc = build_stockham();
-    hipSetDevice(cur);
+    (void)hipSetDevice(cur);
     return rc;
   }
 
@@ -852,7 +852,7 @@ struct PlanImpl final : PlanBase {
     if (!vec_lt<NH>(c, pv) || c == Vec<NH>{}) return NTT_ERR_ARG;
     const std::vector<uint32_t> key(c.begin(), c.end());
     if (key != coset_key) {
-      if (d_coset) hipFree(d_coset);
+      if (d_coset) (void)hipFree(d_coset);
       d_coset = nullptr;
       coset_key.clear();
       std::vector<uint32_t> host;
@@ -926,7 +926,7 @@ struct PlanImpl final : PlanBase {
   int ensure_scratch(unsigned batch) {
     const size_t need = (size_t)n * batch;
     if (need <= scratch_elems) return NTT_OK;
-    if (d_scratch) hipFree(d_scratch);
+    if (d_scratch) (void)hipFree(d_scratch);
     d_scratch = nullptr;
     scratch_elems = 0;
     if (hipMalloc(&d_scratch, need * SCRW * 4) != hipSuccess) return NTT_ERR_HIP;
@@ -985,7 +985,8 @@ struct PlanImpl final : PlanBase {
     };
     if (io && (log_n == 0 || npass == 0)) return NTT_ERR_ARG;  // four-step pieces are >= 8 points
     if (log_n == 0) {
-      if (out != in) hipMemcpyAsync(out, in, (size_t)batch * MEMW * 4, hipMemcpyDeviceToDevice, st);
+      if (out != in && hipMemcpyAsync(out, in, (size_t)batch * MEMW * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return NTT_ERR_HIP;
       return NTT_OK;
     }
     const size_t* off_int = inverse ? off_int_i : off_int_f;
@@ -1281,7 +1282,7 @@ struct PlanImpl final : PlanBase {
     // a mapped piece (the column pieces of ntt_rplan_inverse_cols_piece): the product gathered into a
     // plan-owned buffer first (out's other pieces may still be in flight)
     if (count > pw_elems) {
-      if (d_pw) hipFree(d_pw);
+      if (d_pw) (void)hipFree(d_pw);
       d_pw = nullptr;
       pw_elems = 0;
       if (hipMalloc(&d_pw, count * MEMW * 4) != hipSuccess) return NTT_ERR_HIP;
@@ -1515,10 +1516,10 @@ extern "C++" template <class F>
 static int on_device(ntt_plan* plan, F&& f) {
   if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
   int cur = 0;
-  hipGetDevice(&cur);
-  if (cur != plan->impl->device) hipSetDevice(plan->impl->device);
+  (void)hipGetDevice(&cur);
+  if (cur != plan->impl->device) (void)hipSetDevice(plan->impl->device);
   const int rc = f(*plan->impl);
-  if (cur != plan->impl->device) hipSetDevice(cur);
+  if (cur != plan->impl->device) (void)hipSetDevice(cur);
   return set_err(rc);
 }
 
@@ -1618,12 +1619,12 @@ int ntt_plan_set_profiling(ntt_plan* plan, int enable) {
   PlanBase& P = *plan->impl;
   if (enable && !P.ev[0][0]) {
     int cur = 0;
-    hipGetDevice(&cur);
-    hipSetDevice(P.device);
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(P.device);
     for (auto& row : P.ev)
       for (auto& e : row)
-        if (hipEventCreate(&e) != hipSuccess) { hipSetDevice(cur); return set_err(NTT_ERR_HIP); }
-    hipSetDevice(cur);
+        if (hipEventCreate(&e) != hipSuccess) { (void)hipSetDevice(cur); return set_err(NTT_ERR_HIP); }
+    (void)hipSetDevice(cur);
   }
   P.profiling = enable != 0;
   P.nrec = 0;
@@ -1702,7 +1703,7 @@ static size_t shim_cache_cap() {
 static std::shared_ptr<CachedPlan> cached_plan(const uint64_t* p, const uint64_t* g, unsigned limbs64, unsigned log_n,
                                                int* rc) {
   int dev = 0;
-  hipGetDevice(&dev);
+  (void)hipGetDevice(&dev);
   auto key = std::make_tuple(std::vector<uint64_t>(p, p + limbs64), std::vector<uint64_t>(g, g + limbs64), limbs64,
                              log_n, dev);
   std::lock_guard<std::mutex> lk(g_cache_mu);

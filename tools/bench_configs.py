@@ -65,6 +65,14 @@ def main():
     t = pl.fill(pl.empty(), "random", seed=2)
     emit("C2: 2^20 forward BN254 Fr", 1 << 20, timeit(lambda: pl.forward(t), steps=50), passes=pl.passes)
     del pl, t
+    # C2 as the reference's single-kernel class (NTT_PLAN_SINGLE_LAUNCH: one persistent launch)
+    pl = NTTPlan(1, 20, 4, single_launch=True)
+    t = pl.fill(pl.empty(), "random", seed=2)
+    emit("C2: 2^20 forward BN254 Fr as ONE kernel (NTT_PLAN_SINGLE_LAUNCH)", 1 << 20,
+         timeit(lambda: pl.forward(t), steps=50), passes=pl.passes,
+         note="bit-exact with the 3-launch line above; slower, so a plan flag (DESIGN.md §4)")
+    assert pl.device_status() == 0
+    del pl, t
 
     # C3
     for L in (4, 6):
