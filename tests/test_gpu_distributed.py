@@ -190,21 +190,24 @@ def _dist_worker(rank, world, port, q):
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         log_n = 16
-        d = DistNTT(1, log_n, 4, device=0, host_exchange=True)
-        x = d.fill(d.empty(), "random", seed=8)
-        x0 = x.clone()
-        d.forward(x)
         ref = NTTPlan(1, log_n, 4)
         X = ref.fill(ref.empty(), "random", seed=8)
         ref.forward(X)
-        ok_f = torch.equal(x, X[_index(d.layout, "col")])
-        d.inverse(x)
-        ok_i = torch.equal(x, x0)
-        a, b, c = d.fill(d.empty(), "random", seed=5), d.fill(d.empty(), "random", seed=6), d.empty()
-        d.polymul(a, b, c)
         A, B, C = ref.fill(ref.empty(), "random", seed=5), ref.fill(ref.empty(), "random", seed=6), ref.empty()
         ref.polymul(A, B, C)
-        ok_p = torch.equal(c, C[_index(d.layout, "row")])
+        ok_f = ok_i = ok_p = True
+        # whole blocks, then the two-sided pieces (units exchanged one by one between the processes)
+        for pieces, col_pieces in ((None, None), (2, 4), (4, 2)):
+            d = DistNTT(1, log_n, 4, device=0, host_exchange=True, pieces=pieces, col_pieces=col_pieces)
+            x = d.fill(d.empty(), "random", seed=8)
+            x0 = x.clone()
+            d.forward(x)
+            ok_f = ok_f and torch.equal(x, X[_index(d.layout, "col")])
+            d.inverse(x)
+            ok_i = ok_i and torch.equal(x, x0)
+            a, b, c = d.fill(d.empty(), "random", seed=5), d.fill(d.empty(), "random", seed=6), d.empty()
+            d.polymul(a, b, c)
+            ok_p = ok_p and torch.equal(c, C[_index(d.layout, "row")])
         q.put((rank, ok_f, ok_i, ok_p))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover - reported to the parent
@@ -215,7 +218,7 @@ def test_dist_ntt_two_processes_host_exchange():
     """DistNTT in two processes (ranks 0 and 1 of one transform) on one GPU: rank plans, layouts
     and the exchange schedule of the N > 1 bench path, with the all-to-all staged through host
     memory over gloo (RCCL refuses two ranks on one device).  Forward / inverse / polymul bit-exact
-    against the single-GPU transform."""
+    against the single-GPU transform, with whole blocks and with 2 x 4 and 4 x 2 pieces."""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
