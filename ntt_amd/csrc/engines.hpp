@@ -98,6 +98,7 @@ struct Eng29 {
   // 2^255) need 8 even in the 48-B caller layout, so only the first read and the last write of a
   // transform move 48 B per element
   static constexpr int SCRW = (L <= 9 && W32 > 8) ? 8 : W32;
+  static constexpr int TABW = SCRW;  // words per entry of the element-format twiddle tables
   static constexpr int TW = (2 * L + 3) & ~3;   // words per twiddle-table entry: w, ws (16-B aligned)
   static constexpr int LDSW = L;                // words per element in LDS
   static constexpr int IN = 4;                  // DFT input bound (units of p)
@@ -390,6 +391,9 @@ struct Eng32 {
   // caller's `long long` layout holds 8 (HBM-bound path: a third less traffic per transform).
   // SCR_ != 0 forces the scratch width (EngPI: the caller's 8 B, for NTT_PLAN_IN_PLACE)
   static constexpr int SCRW = SCR_ ? SCR_ : (NTT_P_SCRATCH32 ? 1 : MEMW_);
+  // element-format twiddle tables (w R mod p < 2^31) take 4 B per entry whatever the scratch width:
+  // the in-place plan's pass 1 streams a 2^26-entry table at the SSIP size
+  static constexpr int TABW = 1;
   static constexpr int TW = 2;  // Shoup pair (w, floor(w 2^32 / p))
   static constexpr int LDSW = 1;
   static constexpr int IN = 4;       // bound hints of the generic kernels (every value here is < 2p)
@@ -436,7 +440,7 @@ struct Eng32 {
   }
   template <int MW = MEMW_>
   __device__ static __forceinline__ void load(uint32_t (&x)[W], const uint32_t* __restrict__ base, size_t idx) {
-    static_assert(MW == MEMW_ || MW == SCRW, "HBM width");
+    static_assert(MW == MEMW_ || MW == SCRW || MW == TABW, "HBM width");
     if constexpr (MW == 1)
       x[0] = base[idx];
     else
@@ -446,7 +450,7 @@ struct Eng32 {
   __device__ static __forceinline__ void reduce(uint32_t (&)[W], const Args&) {}  // always < 2p
   template <int MW = MEMW_>
   __device__ static __forceinline__ void put(uint32_t* __restrict__ base, size_t idx, uint32_t v) {
-    static_assert(MW == MEMW_ || MW == SCRW, "HBM width");
+    static_assert(MW == MEMW_ || MW == SCRW || MW == TABW, "HBM width");
     if constexpr (MW == 1)
       base[idx] = v;
     else

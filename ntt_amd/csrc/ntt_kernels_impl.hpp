@@ -528,7 +528,7 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
           // N = s R, input d multiplied by w_N^(c d) -- the same table shape with k = c
           uint32_t tw[E::W];
           const uint32_t k0 = col0 & ((1u << A.lgp) - 1);
-          E::template load<E::SCRW>(tw, A.tw_full, ((size_t)k0 << LOGR) + pi * T + c);
+          E::template load<E::TABW>(tw, A.tw_full, ((size_t)k0 << LOGR) + pi * T + c);
           E::mulv(x[j * Q + d], tw, A.F);
         }
         if constexpr (PRO == PRO_PW) {
@@ -618,7 +618,7 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
 #if NTT_AB_SKIP & 16  // timing-only (tools/r03_ab.sh): the table reads folded into an L2-resident window
               ti &= (size_t(1) << 14) - 1;
 #endif
-              E::template load<E::SCRW>(tw, A.tw_full, NTT_NOMEM(ti));
+              E::template load<E::TABW>(tw, A.tw_full, NTT_NOMEM(ti));
               E::mulv(v, tw, A.F);
             }
           } else {
@@ -644,7 +644,7 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
           }
           if constexpr (EPI) {  // four-step twiddle w_n^(j1 k2) of this output (ntt_rplan), then the pack map
             uint32_t tw[E::W];
-            E::template load<E::SCRW>(tw, A.tw_epi, epi_idx(pos));
+            E::template load<E::TABW>(tw, A.tw_epi, epi_idx(pos));
             E::mulv(v, tw, A.F);
             E::template store<E::MUL_OUT, FAST, DW>(dst, ck(NTT_NOMEM(out_pos(pos)), A.dbg_dst_n), v, A.F);
           } else {
@@ -655,7 +655,7 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
           if constexpr (EPI) {
             if (A.flags & 1u) E::mul(v, A.F.ninv, A.F);
             uint32_t tw[E::W];
-            E::template load<E::SCRW>(tw, A.tw_epi, epi_idx(pos));
+            E::template load<E::TABW>(tw, A.tw_epi, epi_idx(pos));
             E::mulv(v, tw, A.F);
             E::template store<E::MUL_OUT, FAST>(dst, ck(out_pos(pos), A.dbg_dst_n), v, A.F);
           } else if (A.flags & 1u) {
@@ -1013,7 +1013,7 @@ __global__ void k_build_tw(uint32_t* __restrict__ out, size_t count, uint32_t lo
       E::mul(u.w, v, F);
       E::mulv(a.w, u.w, F);
     }
-    E::template store<E::MUL_OUT, false, E::SCRW>(out, idx, a.w, F);  // outer-twiddle tables: E::SCRW words
+    E::template store<E::MUL_OUT, false, E::TABW>(out, idx, a.w, F);  // outer-twiddle tables: E::TABW words
   }
 }
 
@@ -1138,7 +1138,7 @@ __global__ void k_build_fs_tw(uint32_t* __restrict__ out, uint32_t log_rows, uin
     E::tload(x, lo, (uint32_t)(e & ((1ull << lo_bits) - 1)));
     E::tload(y, hi, (uint32_t)(e >> lo_bits));
     E::mul(x.w, y, F);
-    E::template store<E::MUL_OUT, false, E::SCRW>(out, idx, x.w, F);
+    E::template store<E::MUL_OUT, false, E::TABW>(out, idx, x.w, F);
   }
 }
 

@@ -363,7 +363,8 @@ struct PlanImpl final : PlanBase {
   static constexpr int NH = EngHost<E>::NH;
   static constexpr int TW = E::TW;
   static constexpr int MEMW = E::MEMW;
-  static constexpr int SCRW = E::SCRW;  // scratch and outer-twiddle tables (engines.hpp)
+  static constexpr int SCRW = E::SCRW;  // scratch (engines.hpp)
+  static constexpr int TABW = E::TABW;  // element-format twiddle tables (engines.hpp)
   HostField<NH> H;
   EngHost<E> EH;
   typename E::Args Ff{}, Fi{};
@@ -627,13 +628,13 @@ struct PlanImpl final : PlanBase {
         }
         lgp += ri;
       }
-      if (hipMalloc(&d_stk_tab, elems * SCRW * 4) != hipSuccess) return NTT_ERR_HIP;
+      if (hipMalloc(&d_stk_tab, elems * TABW * 4) != hipSuccess) return NTT_ERR_HIP;
       for (auto*& p : d_stk_buf)
         if (hipMalloc(&p, (size_t)n * MEMW * 4) != hipSuccess) return NTT_ERR_HIP;
       lgp = r[stk_ord[0]];
       for (unsigned i = 1; i < npass; ++i) {
         const unsigned ri = r[stk_ord[i]];
-        if (launch_build_tw<E>(d_stk_tab + stk_off[i] * SCRW, 1ull << (lgp + ri), ri, tl - ri, log_n - lgp - ri,
+        if (launch_build_tw<E>(d_stk_tab + stk_off[i] * TABW, 1ull << (lgp + ri), ri, tl - ri, log_n - lgp - ri,
                                d_tab + off_los_f, d_tab + off_hi_f, lo_bits, Ff, nullptr) != hipSuccess)
           return NTT_ERR_HIP;
         lgp += ri;
@@ -672,7 +673,7 @@ struct PlanImpl final : PlanBase {
                                (uint32_t)(blocks - b0 < chunk ? blocks - b0 : chunk), st);
           }
         } else {
-          A.tw_full = d_stk_tab + stk_off[i] * SCRW;  // w_N^(c d), N = 2^(lgp + r_i)
+          A.tw_full = d_stk_tab + stk_off[i] * TABW;  // w_N^(c d), N = 2^(lgp + r_i)
           A.log_blk = lgp + ri;
           A.lgp = lgp;
           A.src_user = 1;
@@ -694,7 +695,7 @@ struct PlanImpl final : PlanBase {
       const unsigned ri = r[stk_ord[i]];
       PassArgs<E> A = base_args(false);
       A.tw_int = d_tab + off_int_f[stk_ord[i]];  // w_R^e for this pass's radix
-      A.tw_full = i ? d_stk_tab + stk_off[i] * SCRW : nullptr;
+      A.tw_full = i ? d_stk_tab + stk_off[i] * TABW : nullptr;
       A.log_blk = log_n;
       A.lgp = lgp;
       A.src_user = 1;
@@ -723,7 +724,7 @@ struct PlanImpl final : PlanBase {
     full_elems = elems;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return NTT_OK;
-    if (2 * elems * SCRW * 4 > free_b / 4) return NTT_OK;  // both directions within a quarter of free HBM
+    if (2 * elems * TABW * 4 > free_b / 4) return NTT_OK;  // both directions within a quarter of free HBM
     if (int rc = ensure_full(0)) return rc;
     use_full = true;
     return build_shoup_tables();
@@ -731,7 +732,7 @@ struct PlanImpl final : PlanBase {
   // the per-pass tables of one direction (the inverse's pass-1 table carries n^-1)
   int ensure_full(int dir) {
     if (d_fulls[dir]) return NTT_OK;
-    if (hipMalloc(&d_fulls[dir], full_elems * SCRW * 4) != hipSuccess) {
+    if (hipMalloc(&d_fulls[dir], full_elems * TABW * 4) != hipSuccess) {
       d_fulls[dir] = nullptr;
       return NTT_ERR_HIP;
     }
@@ -740,7 +741,7 @@ struct PlanImpl final : PlanBase {
       const uint32_t* lo = d_tab + (dir ? off_los_i : off_los_f);
       const uint32_t* hi = d_tab + (dir ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
       // column-group-major layout of the pass kernel's tiles (T = TILE / R columns per workgroup)
-      if (launch_build_tw<E>(d_fulls[dir] + full_off[i] * SCRW, 1ull << blk, r[i], tile_log_of<E>() - r[i], log_n - blk,
+      if (launch_build_tw<E>(d_fulls[dir] + full_off[i] * TABW, 1ull << blk, r[i], tile_log_of<E>() - r[i], log_n - blk,
                              lo, hi, lo_bits, dir ? Fi : Ff, nullptr) != hipSuccess)
         return NTT_ERR_HIP;
       blk -= r[i];
@@ -902,7 +903,7 @@ struct PlanImpl final : PlanBase {
   // w_n^(col k) c^col R_e, layout of d_full (built on the device once per shift).
   int ensure_coset_full() {
     if (coset_full_ok) return NTT_OK;
-    if (!d_coset_full && hipMalloc(&d_coset_full, (size_t)n * SCRW * 4) != hipSuccess) {
+    if (!d_coset_full && hipMalloc(&d_coset_full, (size_t)n * TABW * 4) != hipSuccess) {
       d_coset_full = nullptr;
       return NTT_ERR_HIP;
     }
@@ -1035,7 +1036,7 @@ struct PlanImpl final : PlanBase {
           const char* v = getenv("NTT_PASS1_FULL");
           return v && atoi(v) > 0;
         }();
-        A.tw_full = (use_full && (i > 0 || E::PASS1_FULL_TABLE || p1_full)) ? d_fulls[inverse ? 1 : 0] + full_off[i] * SCRW
+        A.tw_full = (use_full && (i > 0 || E::PASS1_FULL_TABLE || p1_full)) ? d_fulls[inverse ? 1 : 0] + full_off[i] * TABW
                                                                              : nullptr;
         if (i > 0 && d_full_sh && full_sh_ok[i]) {
           A.tw_full = d_full_sh + full_sh_off[inverse ? 1 : 0][i] * TW;
@@ -1310,7 +1311,7 @@ struct PlanImpl final : PlanBase {
                : NTT_ERR_HIP;
   }
 
-  size_t table_entry_bytes() const override { return (size_t)SCRW * 4; }
+  size_t table_entry_bytes() const override { return (size_t)TABW * 4; }
 
   // Fused polymul is available for multi-pass FAST plans with full outer-twiddle tables.
   bool polymul_fusable() const {
@@ -1324,7 +1325,7 @@ struct PlanImpl final : PlanBase {
   int ensure_polymul_table() {
     if (d_full_pm) return NTT_OK;
     const size_t elems = 1ull << log_n;
-    if (hipMalloc(&d_full_pm, elems * SCRW * 4) != hipSuccess) {
+    if (hipMalloc(&d_full_pm, elems * TABW * 4) != hipSuccess) {
       d_full_pm = nullptr;
       return NTT_ERR_HIP;
     }

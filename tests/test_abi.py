@@ -91,6 +91,18 @@ def test_mplan_create_fails_cleanly_without_gpu_or_bad_args():
     assert so.ntt_mplan_destroy(None) == 0
 
 
+def test_piece_entry_points_reject_null_plans_without_gpu():
+    """The two-sided piece entry points (ntt_rplan_*_piece, ntt_mplan_set_pieces2) check their plan
+    before touching a device."""
+    from ntt_amd import lib as L
+    so = L.load()
+    assert so.ntt_rplan_forward_rows_piece(None, None, None, 1, 0, 0, 1, 1, None) == -1
+    assert so.ntt_rplan_forward_cols_piece(None, None, None, 1, 0, 0, 1, 1, None) == -1
+    assert so.ntt_rplan_inverse_cols_piece(None, None, None, None, 0, 1, 1, None) == -1
+    assert so.ntt_rplan_inverse_rows_piece(None, None, None, 0, 1, 1, None) == -1
+    assert so.ntt_mplan_set_pieces2(None, 1, 1) == -1
+
+
 def test_limb_counts_outside_1_4_6_are_rejected_before_any_packing():
     """limbs64 >= 7 used to overrun the 12-word modulus buffers; now NTT_ERR_ARG."""
     from ntt_amd import lib as L

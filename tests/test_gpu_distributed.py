@@ -63,6 +63,31 @@ def test_virtual_ranks_match_single_gpu(world, log_n, field_id, L, pieces, col_p
         assert torch.equal(s, t)
 
 
+def test_piece_entry_points_reject_bad_pieces():
+    """ntt_rplan_*_piece: piece counts must be powers of two within the rows / columns and the piece
+    index within its count; ntt_mplan_set_pieces2 likewise (NTT_ERR_ARG, nothing launched)."""
+    import ctypes as C
+    from ntt_amd import lib as L
+    from ntt_amd.distributed import MultiPlan, RankPlan
+    lib = L.load()
+    rp = RankPlan(1, 12, 4, 2, 0, 0)  # rank 0 of 2; the split is read from the plan
+    lay = rp.layout
+    x, send = rp.empty(lay.local_n), rp.empty(lay.local_n)
+    p = lambda t: C.c_void_p(t.data_ptr())
+    h = rp.handle
+    assert lib.ntt_rplan_forward_rows_piece(h, p(x), p(send), 1, 0, 0, 3, 1, None) == -1          # not 2^k
+    assert lib.ntt_rplan_forward_rows_piece(h, p(x), p(send), 1, 0, 2, 2, 1, None) == -1          # index >= count
+    assert lib.ntt_rplan_forward_rows_piece(h, p(x), p(send), 1, 0, 0, 2 * lay.r, 1, None) == -1  # > r rows
+    assert lib.ntt_rplan_forward_cols_piece(h, p(send), p(x), 1, 0, 0, 1, 2 * lay.c, None) == -1  # > c columns
+    assert lib.ntt_rplan_inverse_cols_piece(h, p(x), None, p(send), 4, 1, 4, None) == -1
+    assert lib.ntt_rplan_inverse_rows_piece(h, p(send), p(x), 0, 0, 1, None) == -1                # zero pieces
+    assert lib.ntt_rplan_forward_rows_piece(h, p(x), p(send), 3, 0, 0, 1, 1, None) == -1          # nvec 3
+    mp = MultiPlan(1, 12, 4, devices=[0])
+    assert lib.ntt_mplan_set_pieces2(mp.handle, 3, 1) == -1
+    assert lib.ntt_mplan_set_pieces2(mp.handle, 1, 32) == -1
+    assert lib.ntt_mplan_set_pieces2(mp.handle, 2, 2) == 0
+
+
 def test_rank_plan_split_takes_fewest_passes():
     """ntt_rplan_create's split: balanced unless a narrower n2 saves a pass kernel (2^24 BN254:
     14 + 10 = 2 + 1 passes instead of 12 + 12 = 2 + 2; 2^20 keeps 10 + 10; C4's 2^28 keeps 14 + 14,
