@@ -31,6 +31,11 @@ namespace ntt {
 #else
 #define NTT_NOMEM(i) (i)
 #endif
+// Timing experiments only: wave priority (s_setprio) for a tile's load phase (bit 0; bit 2:
+// not in a pass that reads the caller's buffer) and for its output phase (bit 1).
+#ifndef NTT_PRIO
+#define NTT_PRIO 0
+#endif
 
 // Compile-time loop: f(std::integral_constant<int, I>{}) for I in [0, N).  Register arrays indexed
 // by I stay in VGPRs (a loop the unroller gives up on would send x[][] to scratch).
@@ -390,6 +395,13 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
   int t = threadIdx.x;
   if constexpr (LOOPED) asm volatile("" : "+v"(t));
   if (t >= NT) return;
+#if NTT_PRIO & 1
+  // timing experiment: a new tile's address math and loads issue ahead of older waves' compute
+  __builtin_amdgcn_s_setprio(2);
+#elif NTT_PRIO & 4
+  // the same except in a pass that reads the caller's buffer (pass 1: it measured slower there)
+  if (!(KIND == KIND_COLUMN && A.src_user)) __builtin_amdgcn_s_setprio(2);
+#endif
   // Four-step addressing (PassArgs::fs, ntt_rplan_*): the first pass may read and the last pass may
   // write through the per-peer chunk maps, and Mode I runs 2^il interleaved transforms.  All flags
   // are kernel arguments (wave-uniform branches); fs == 0 is the plain batched transform.
@@ -542,6 +554,9 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
         }
       });
     });
+#if NTT_PRIO & 5
+    __builtin_amdgcn_s_setprio(0);  // the tile's loads are issued
+#endif
     static_for<G>([&](auto J) {
       constexpr int j = J;
       dft<E, Q, j * Q, FAST>(x, A.F);
@@ -575,6 +590,9 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
 
   // ------------------------------------------------------------------ output
   if constexpr (IPN) ipn_wait_mirror(A, midrev);  // the slab this tile writes into has been read
+#if NTT_PRIO & 2
+  __builtin_amdgcn_s_setprio(1);  // timing experiment: finishing tiles drain first
+#endif
   {
     constexpr int ls = S::nsub - 1;
     constexpr int qb = S::qb(ls), Q = 1 << qb, G = EPT / Q, sb = S::logsig(ls), lN = S::logN(ls);
