@@ -1,6 +1,7 @@
 """The multi-GPU four-step schedule (ntt_amd.distributed.FourStep) on CPU: gloo all-to-all with
-world_size 2 and 4, local steps done by an oracle-backed test engine.  Checks the layouts, the
-twiddle/pack index math and the exchange against the single-transform oracle."""
+world_size 2, 4 and 8 (8: the rank count of the N = 8 bench line), local steps done by an
+oracle-backed test engine.  Checks the layouts, the twiddle/pack index math and the exchange
+against the single-transform oracle."""
 import os
 import socket
 
@@ -59,7 +60,7 @@ def _worker(rank, world, port, field_id, log_n, L, q, pieces=1, log_n2=None, col
                          [(2, 1, 6, 1, None, 1), (2, 2, 7, 1, None, 1), (4, 1, 8, 1, None, 1), (2, 1, 6, 2, None, 1),
                           (2, 2, 7, 3, None, 1), (4, 1, 8, 4, None, 1), (2, 1, 8, 2, 3, 1), (4, 2, 9, 1, 3, 1),
                           (2, 1, 8, 1, None, 4), (2, 1, 8, 2, None, 2), (4, 1, 10, 4, None, 2),
-                          (2, 2, 9, 4, 4, 8)])
+                          (2, 2, 9, 4, 4, 8), (8, 1, 8, 1, None, 1), (8, 2, 10, 2, None, 2)])
 def test_four_step_gloo(world, field_id, log_n, pieces, log_n2, col_pieces):
     """pieces / col_pieces > 1: the pipelined schedule (the all-to-all in row-piece x column-piece
     units overlapping the row transforms before it and the column transforms after it; a count that
@@ -141,7 +142,8 @@ def _polymul_worker(rank, world, port, field_id, log_n, L, square, q, pieces=1, 
 @pytest.mark.parametrize("world,field_id,log_n,square,pieces,log_n2,col_pieces",
                          [(2, 1, 6, False, 1, None, 1), (4, 1, 8, False, 1, None, 1), (2, 2, 7, True, 1, None, 1),
                           (2, 1, 6, False, 2, None, 1), (4, 1, 8, False, 4, None, 1), (2, 2, 7, True, 2, None, 1),
-                          (2, 1, 8, False, 2, 3, 1), (2, 1, 8, False, 2, None, 4), (4, 2, 10, True, 2, None, 2)])
+                          (2, 1, 8, False, 2, 3, 1), (2, 1, 8, False, 2, None, 4), (4, 2, 10, True, 2, None, 2),
+                          (8, 1, 8, False, 1, None, 1)])
 def test_distributed_polymul_gloo(world, field_id, log_n, square, pieces, log_n2, col_pieces):
     """C5's schedule (forward(a), forward(b) in ONE all-to-all, local pointwise product fused into
     the inverse, inverse all-to-all) over gloo: the row-layout result equals the oracle's cyclic
