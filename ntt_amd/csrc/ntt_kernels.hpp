@@ -132,14 +132,17 @@ struct FusedArgs {
   uint32_t rbase;              // ready word of counter i at sync[rbase + 32 i] (one 128-B line each)
   uint32_t dbg;                // diagnostics only (NTT_FUSED_DBG): bit 0 no dependency waits (wrong
                                // output), bit 2 static tile order (needs every workgroup resident)
+  uint32_t mode;               // 0: dataflow hand-offs between tiles (k_fused3); 1: two grid barriers
+                               // over a cooperative launch (k_fused3b)
 };
 template <class E>
 hipError_t launch_fused3(int r1, int r2, int r3, const uint32_t* src, uint32_t* scratch, uint32_t* dst,
                          const PassArgs<E>& A1, const PassArgs<E>& A2, const PassArgs<E>& A3, const FusedArgs& F,
                          hipStream_t st);
-// workgroups one launch of k_fused3<E, r1, r2, r3> keeps resident on `device` (occupancy query x CUs)
+// workgroups one launch of k_fused3<E, r1, r2, r3> (mode 0) or k_fused3b (mode 1) keeps resident on
+// `device` (occupancy query x CUs)
 template <class E>
-hipError_t fused3_capacity(int r1, int r2, int r3, int device, uint32_t* wgs);
+hipError_t fused3_capacity(int r1, int r2, int r3, int device, uint32_t* wgs, uint32_t mode = 0);
 
 // The in-place final pass with the digit reversal fused (NTT_PLAN_IN_PLACE, batch 1): A.ipn_* set,
 // grid = n / TILE workgroups, src == dst.  See k_final_ipn.

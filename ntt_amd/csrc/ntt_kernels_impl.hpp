@@ -17,6 +17,7 @@
 // radix-2 rounds (SSIP_NTT_stage1 GZKP-NTT.cu:1297-1357) and its cub::WarpExchange /
 // parallel-load staging (test-cub-WarpExchange.cu:6-64, parallel-load.cu:114-193).
 #pragma once
+#include <cstdlib>
 #include <utility>
 
 #include "ntt_kernels.hpp"
@@ -327,11 +328,11 @@ __device__ __forceinline__ void ipn_signal_read(const PassArgs<E>& A, uint32_t m
 template <class E>
 __device__ __forceinline__ void ipn_wait_mirror(const PassArgs<E>& A, uint32_t midrev) {
   if (threadIdx.x == 0) {
-    uint32_t* ready = A.ipn_sync + 32 * (1 + midrev) + 1;
+    // relaxed global loads of the ready word (no read-modify-write polls: DESIGN §4)
+    typedef __attribute__((address_space(1))) uint32_t gu32;
+    gu32* const ready = (gu32*)(A.ipn_sync + 32 * (1 + midrev) + 1);
     for (uint32_t spins = 0;; ++spins) {
-      uint32_t v = 1u;
-      __hip_atomic_compare_exchange_strong(ready, &v, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (v) break;
+      if (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
       if (spins < 8) __builtin_amdgcn_s_sleep(4);
       else __builtin_amdgcn_s_sleep(32);
       if (spins == (1u << 21)) {  // ~2 s: give up (watchdog word; the output is then wrong)
@@ -801,19 +802,17 @@ __device__ __forceinline__ void fused_publish(uint32_t* cnt, uint32_t* ready, ui
   if (threadIdx.x == 0 && __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == need - 1)
     __hip_atomic_store(ready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// Consumer: one lane polls the ready word (an atomic compare-exchange, performed where the atomic
-// store landed), sleeping 60 ns .. 1 us between polls; then ONE agent-scope acquire, its wait, and
+// Consumer: one lane polls the ready word with relaxed agent-scope loads (compare-exchange polls,
+// read-modify-writes at the memory side, queued the producers' updates behind them: 2^20 single
+// launch 0.162 -> see DESIGN §4), sleeping 60 ns .. 1 us between polls; then ONE agent-scope acquire, its wait, and
 // the workgroup barrier before any load of the handed-off tile.  Bounded: after ~2 s it gives up and
 // raises the watchdog word (the output is then wrong; every wave still reaches the exit).
 __device__ __forceinline__ void fused_wait(uint32_t* ready, uint32_t* watchdog, uint32_t dbg) {
   if (dbg & 1u) return;  // diagnostics only: no dependency waits (wrong output)
   if (threadIdx.x == 0) {
-    uint32_t spins = 0;
-    for (;;) {
-      uint32_t v = 1u;
-      __hip_atomic_compare_exchange_strong(ready, &v, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-      if (v) break;
+    typedef __attribute__((address_space(1))) uint32_t gu32;  // a global (not flat) access
+    gu32* const g = (gu32*)ready;
+    for (uint32_t spins = 0; __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;) {
       if (spins < 4) __builtin_amdgcn_s_sleep(2);
       else if (spins < 16) __builtin_amdgcn_s_sleep(8);
       else __builtin_amdgcn_s_sleep(32);
@@ -917,6 +916,82 @@ void k_fused3(const FusedKArgs<E> K) {
   }
 }
 
+// The same three passes with two grid-wide barriers instead of per-tile hand-offs (FusedArgs::mode 1,
+// a cooperative launch, so every workgroup is resident).  Each workgroup runs tiles b, b + G, ... of a
+// pass, then the barrier.  The barrier (the guide's R1 publish, MI355X_MICROARCH.md § visibility):
+// * scratch stores are write-through (sc1), so no release fence: every wave drains them, then a
+//   workgroup barrier, then one lane counts the workgroup in;
+// * the last of the G arrivals raises the barrier's go word (its own 128-B line);
+// * one lane per workgroup polls that word with relaxed global loads (bounded: then the watchdog
+//   word), takes ONE agent-scope acquire, and the workgroup barrier releases every wave.
+// A/B: plain stores with an agent-scope release per workgroup were slower at 2^20
+// (every release writes back its XCD's L2), and compare-exchange polls of one word by 1024
+// workgroups made each barrier cost ~0.15 ms.
+// The arrival counter is cumulative (barrier k completes at k G arrivals); the last workgroup out
+// re-zeroes the words for the next launch.
+__device__ __forceinline__ void fused_grid_barrier(const FusedArgs& F, uint32_t k) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores are done
+  __syncthreads();
+  uint32_t* const go = F.sync + F.rbase + 32 * (k - 1);
+  if (threadIdx.x == 0) {
+    if (__hip_atomic_fetch_add(F.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k * gridDim.x - 1)
+      __hip_atomic_store(go, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // poll the go word with relaxed agent-scope loads (global, not flat), bounded like fused_wait
+    typedef __attribute__((address_space(1))) uint32_t gu32;
+    gu32* const g = (gu32*)go;
+    for (uint32_t spins = 0; __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;) {
+      if (spins < 16) __builtin_amdgcn_s_sleep(4);
+      else __builtin_amdgcn_s_sleep(32);
+      if (++spins == (1u << 21)) {
+        __hip_atomic_store(F.sync + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+template <class E, int R1, int R2, int R3>
+__global__ __launch_bounds__((1 << E::TILE_LOG) / E::EPT) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
+void k_fused3b(const FusedKArgs<E> K) {
+  static_assert(E::FASTRED && E::SHOUP_OUTER && !E::LDS_TW, "fused schedule: FAST 256-bit engines");
+  constexpr int LW = pass_lds_words<E, R1, KIND_COLUMN>();
+  static_assert(LW == pass_lds_words<E, R3, KIND_FINAL>(), "one tile size");
+  __shared__ __attribute__((aligned(16))) uint32_t lds[LW];
+  __shared__ uint32_t lds_tw[1];
+  const FusedArgs& F = K.F;
+  const uint32_t G = gridDim.x;
+  for (uint32_t w = blockIdx.x; w < F.tiles; w += G) {  // pass 1: the caller's buffer -> scratch
+    const FusedKArgs<E>& L = fused_kargs<E>();
+    pass_tile<E, R1, KIND_COLUMN, true, true, PRO_NONE, true, 0, false, true, true>(L.src, L.scratch, L.A1,
+                                                                                                w, 0, lds, lds_tw);
+    __syncthreads();  // every wave is done with this tile's LDS
+  }
+  fused_grid_barrier(F, 1);
+  for (uint32_t w = blockIdx.x; w < F.tiles; w += G) {  // pass 2: scratch in place
+    const FusedKArgs<E>& L = fused_kargs<E>();
+    pass_tile<E, R2, KIND_COLUMN, true, true, PRO_NONE, true, 0, true, true, true>(L.scratch, L.scratch, L.A2,
+                                                                                               w, 0, lds, lds_tw);
+    __syncthreads();
+  }
+  fused_grid_barrier(F, 2);
+  for (uint32_t w = blockIdx.x; w < F.tiles; w += G) {  // final pass: scratch -> the caller's buffer
+    const FusedKArgs<E>& L = fused_kargs<E>();
+    pass_tile<E, R3, KIND_FINAL, false, true, PRO_NONE, true, 0, false, false, true>(L.scratch, L.dst, L.A3, w, 0,
+                                                                                       lds, lds_tw);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && __hip_atomic_fetch_add(F.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
+    // the last workgroup out: every other one has passed both barriers
+    __hip_atomic_store(F.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(F.sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(F.sync + F.rbase, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(F.sync + F.rbase + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <class E>
 hipError_t launch_fused3(int r1, int r2, int r3, const uint32_t* src, uint32_t* scratch, uint32_t* dst,
                          const PassArgs<E>& A1, const PassArgs<E>& A2, const PassArgs<E>& A3, const FusedArgs& F,
@@ -925,9 +1000,22 @@ hipError_t launch_fused3(int r1, int r2, int r3, const uint32_t* src, uint32_t* 
     return hipErrorInvalidValue;
   } else {
     const dim3 g(F.nwg), b((1 << E::TILE_LOG) / E::EPT);
+    FusedKArgs<E> K{src, scratch, dst, A1, A2, A3, F};
+    void* kargs[] = {&K};
+    static const bool coop = [] {  // NTT_FUSED_COOP=0: a plain launch of the grid-barrier form (A/B)
+      const char* v = getenv("NTT_FUSED_COOP");
+      return !(v && *v == '0');
+    }();
+    // mode 1: a cooperative launch (every workgroup resident, or the launch fails: never a hang)
 #define NTT_FUSED_CASE(a, c, d)                                                                   \
   if (r1 == a && r2 == c && r3 == d) {                                                            \
-    hipLaunchKernelGGL((k_fused3<E, a, c, d>), g, b, 0, st, FusedKArgs<E>{src, scratch, dst, A1, A2, A3, F});    \
+    if (F.mode == 1 && coop)                                                                      \
+      return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_fused3b<E, a, c, d>), g, b, kargs, 0, st); \
+    if (F.mode == 1) {                                                                            \
+      hipLaunchKernelGGL((k_fused3b<E, a, c, d>), g, b, 0, st, K);                                \
+      return hipGetLastError();                                                                   \
+    }                                                                                             \
+    hipLaunchKernelGGL((k_fused3<E, a, c, d>), g, b, 0, st, K);                                   \
     return hipGetLastError();                                                                     \
   }
     NTT_FUSED_CASE(6, 6, 6)
@@ -943,7 +1031,7 @@ hipError_t launch_fused3(int r1, int r2, int r3, const uint32_t* src, uint32_t* 
 }
 
 template <class E>
-hipError_t fused3_capacity(int r1, int r2, int r3, int device, uint32_t* wgs) {
+hipError_t fused3_capacity(int r1, int r2, int r3, int device, uint32_t* wgs, uint32_t mode) {
   if constexpr (!(E::FASTRED && E::SHOUP_OUTER && !E::LDS_TW && E::TILE_LOG == 10 && E::EPT == 4)) {
     return hipErrorInvalidValue;
   } else {
@@ -953,8 +1041,10 @@ hipError_t fused3_capacity(int r1, int r2, int r3, int device, uint32_t* wgs) {
     hipError_t e = hipErrorInvalidValue;
 #define NTT_FUSED_OCC(a, c, d)                                                                         \
   if (r1 == a && r2 == c && r3 == d)                                                                   \
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_fused3<E, a, c, d>), \
-                                                     threads, 0);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(                                                   \
+        &per, mode == 1 ? reinterpret_cast<const void*>(&k_fused3b<E, a, c, d>)                        \
+                        : reinterpret_cast<const void*>(&k_fused3<E, a, c, d>),                        \
+        threads, 0);
     NTT_FUSED_OCC(6, 6, 6)
     NTT_FUSED_OCC(7, 6, 6)
     NTT_FUSED_OCC(7, 7, 6)
@@ -1654,7 +1744,7 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
 #define NTT_INSTANTIATE_FUSED(E)                                                                                  \
   template hipError_t launch_fused3<E>(int, int, int, const uint32_t*, uint32_t*, uint32_t*, const PassArgs<E>&,     \
                                        const PassArgs<E>&, const PassArgs<E>&, const FusedArgs&, hipStream_t);      \
-  template hipError_t fused3_capacity<E>(int, int, int, int, uint32_t*);
+  template hipError_t fused3_capacity<E>(int, int, int, int, uint32_t*, uint32_t);
 
 #define NTT_INSTANTIATE(E)                                                                                         \
   NTT_EXTERN_KIND(E, KIND_COLUMN)                                                                                  \

@@ -1158,8 +1158,13 @@ struct PlanImpl final : PlanBase {
     } else {
     if (npass != 3 || !use_full || !d_full_sh || !full_sh_ok[1] || !Ff.red_ok) return false;
     const unsigned tl = tile_log_of<E>();
+    // NTT_FUSED_MODE=0: the dataflow form (per-tile hand-offs), =1: the grid-barrier form
+    static const uint32_t mode = [] {
+      const char* v = getenv("NTT_FUSED_MODE");
+      return v && *v ? (uint32_t)atoi(v) : 1u;
+    }();
     uint32_t cap = 0;
-    if (fused3_capacity<E>((int)r[0], (int)r[1], (int)r[2], device, &cap) != hipSuccess || cap == 0) return false;
+    if (fused3_capacity<E>((int)r[0], (int)r[1], (int)r[2], device, &cap, mode) != hipSuccess || cap == 0) return false;
     const unsigned r1 = r[0], r2 = r[1], r3 = r[2];
     const unsigned lt1 = tl - r1, lt2 = tl - r2, lt3 = tl - r3, lu = lt1 > lt2 ? lt1 : lt2;
     if (r3 < lu || r1 < lt3) return false;  // schedule_ok guarantees both; kept as the kernel's contract
@@ -1176,6 +1181,10 @@ struct PlanImpl final : PlanBase {
     F.n23 = 1u << (r1 - lt3);
     F.need12 = 1u << (lu - lt1 + r2);
     F.need23 = 1u << r2;
+    F.mode = mode;
+    if (getenv("NTT_FUSED_VERBOSE"))
+      fprintf(stderr, "libntt: fused schedule mode %u, %u tiles per pass, %u workgroups (capacity %u)\n", mode, F.tiles,
+              F.nwg, cap);
     if (const char* v = getenv("NTT_FUSED_DBG")) F.dbg = (uint32_t)atoi(v);
     F.rbase = (4 + F.n12 + F.n23 + 31) & ~31u;
     const size_t words = F.rbase + 32 * (F.n12 + F.n23);
