@@ -1158,11 +1158,10 @@ struct PlanImpl final : PlanBase {
     } else {
     if (npass != 3 || !use_full || !d_full_sh || !full_sh_ok[1] || !Ff.red_ok) return false;
     const unsigned tl = tile_log_of<E>();
-    // NTT_FUSED_MODE=0: the dataflow form (per-tile hand-offs), =1: the grid-barrier form
-    static const uint32_t mode = [] {
-      const char* v = getenv("NTT_FUSED_MODE");
-      return v && *v ? (uint32_t)atoi(v) : 1u;
-    }();
+    // NTT_FUSED_MODE=0: the dataflow form (per-tile hand-offs), =1: the grid-barrier form (default);
+    // read when the plan builds its fused schedule (its first single-launch call)
+    const char* mv = getenv("NTT_FUSED_MODE");
+    const uint32_t mode = (mv && *mv == '0') ? 0u : 1u;
     uint32_t cap = 0;
     if (fused3_capacity<E>((int)r[0], (int)r[1], (int)r[2], device, &cap, mode) != hipSuccess || cap == 0) return false;
     const unsigned r1 = r[0], r2 = r[1], r3 = r[2];

@@ -1,6 +1,7 @@
 """BASELINE config 2 as a single kernel (VERDICT r02 missing 1): NTT_PLAN_SINGLE_LAUNCH runs a 3-pass
-transform as ONE persistent launch (k_fused3: the passes' tiles handed between workgroups through
-dependency counters).  Checked bit for bit against the threaded C oracle (GZKP-NTT.cu:30-48, inverse
+transform as ONE persistent launch, in both forms (NTT_FUSED_MODE, read when a plan builds its fused
+schedule): "1" two grid barriers over a cooperative launch (k_fused3b, the default), "0" the passes'
+tiles handed between workgroups through dependency counters (k_fused3).  Checked bit for bit against the threaded C oracle (GZKP-NTT.cu:30-48, inverse
 GZKP-NTT.cu:1725-1732) at C2's 2^20 on vectors A (x_j = j, the reference's input) and B, against the
 default 3-launch schedule at every fused size 2^18..2^24 for BN254 and BLS12-381 (4 limbs), over
 repeated calls (the counters re-zero themselves), and that exactly one launch ran with the watchdog
@@ -27,8 +28,14 @@ def _host(t):
     return t.cpu().numpy().view(np.uint64).reshape(-1, 4)
 
 
+@pytest.fixture(params=["1", "0"], ids=["barriers", "dataflow"])
+def fused_mode(request, monkeypatch):
+    monkeypatch.setenv("NTT_FUSED_MODE", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("kind", ["iota", "random"])
-def test_c2_2pow20_single_launch_vs_oracle(kind):
+def test_c2_2pow20_single_launch_vs_oracle(kind, fused_mode):
     fid, log_n = 1, 20
     p, g = R.FIELDS[fid]
     pl = _plan(fid, log_n, True)
@@ -54,7 +61,7 @@ def test_c2_2pow20_single_launch_vs_oracle(kind):
 
 @pytest.mark.parametrize("fid", [1, 2])
 @pytest.mark.parametrize("log_n", [18, 19, 20, 21, 22, 23, 24])
-def test_single_launch_matches_default_schedule(fid, log_n):
+def test_single_launch_matches_default_schedule(fid, log_n, fused_mode):
     ref = _plan(fid, log_n, False)
     fused = _plan(fid, log_n, True)
     assert ref.passes == fused.passes and len(fused.passes) == 3
