@@ -99,10 +99,11 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
 #define NTT_PLAN_IN_PLACE 16u
 /* Single-launch schedule (BASELINE config 2, "single-kernel self-sort-in-place"; the reference runs
  * 2^20 as 4 launches, GZKP-NTT.cu:1509-1545): a 3-pass forward / inverse of a 4-limb BN254 / BLS12-381
- * plan (2^18 .. 2^24) runs as ONE persistent launch; the passes' tiles are handed between workgroups
- * through dependency counters instead of kernel boundaries (k_fused3).  Same contract and results as
- * the default schedule; batch 1; other plans and calls ignore the flag.  ntt_plan_device_status
- * reports a dependency wait that gave up (a watchdog; never expected). */
+ * plan (2^18 .. 2^24) runs as ONE persistent launch: two grid-wide barriers in a cooperative launch
+ * (k_fused3b; the default) or the passes' tiles handed between workgroups through dependency
+ * counters (k_fused3; environment NTT_FUSED_MODE=0), instead of kernel boundaries.  Same contract
+ * and results as the default schedule; batch 1; other plans and calls ignore the flag.
+ * ntt_plan_device_status reports a wait that gave up (a watchdog; never expected). */
 #define NTT_PLAN_SINGLE_LAUNCH 32u
 int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags);
 /* Device-side status of a plan since the last call (blocking; clears it).  *bad bit 0: an
