@@ -7,10 +7,18 @@ A "step" is one forward transform of a whole 2^24-element vector (SURVEY §8d sy
 SplitMix64 limbs), resident in HBM when the timed region starts.
 
 * N = 1: one MI355X, one 2^24 transform per step.
-* N > 1 (torch.distributed.run, one rank per GPU): by default ONE 2^24 transform split over the N
-  ranks as the four-step with the RCCL all-to-all ("scaling": "strong"; `value` =
-  2^24 / t, t = max over ranks).  ``--independent`` instead runs one 2^24 transform per rank with no
-  data-path collective ("weak", `value` = N 2^24 / t): a secondary line, linear by construction.
+* N > 1, one rank per GPU: by default ONE 2^24 transform split over the N ranks as the four-step
+  with the RCCL all-to-all ("scaling": "strong"; `value` = 2^24 / t, t = max over
+  ranks).  ``--independent`` instead runs one 2^24 transform per rank with no data-path collective
+  ("weak", `value` = N 2^24 / t): a secondary line, linear by construction.
+  Launch: under ``torch.distributed.run`` (WORLD_SIZE set) every process is one rank.  A plain
+  ``python bench.py --gpus N`` spawns the N ranks itself (torch.distributed.run in a child process,
+  before any GPU call), passes rank 0's line through and exits with the children's status; it
+  refuses N above the visible device count (except the one-GPU rehearsal, NTT_BENCH_EXCHANGE=host).
+  The line carries `rccl_ranks` (world size of the RCCL group), `exchange_ms` /
+  `exchange_gbps_per_link` (bytes each rank sends one peer per exchange / the all-to-all window) and
+  `parity`: after the timed region, the transform's output gathered to rank 0 is compared element by
+  element with a one-GPU plan there, plus the closed-form KAT of x_j = j at sampled k.
 * ``--four-step`` at N = 1 times the partitioned schedule on one GPU (RCCL world size 1);
   ``--log-n 28 --four-step`` on 8 GPUs is BASELINE config 4.
 
@@ -80,12 +88,14 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--four-step", "--dist", dest="four_step", action="store_true",
                     help="one transform split over all ranks (four-step + RCCL all-to-all); default for N > 1")
-    ap.add_argument("--pieces", type=int, default=None,
+    ap.add_argument("--pieces", default=None,
                     help="four-step: row pieces whose all-to-all overlaps the next piece's row transforms "
-                         "(default: DistNTT.auto_pieces, >= 2^22 elements per piece)")
-    ap.add_argument("--col-pieces", type=int, default=None,
+                         "(default 1: one whole-block exchange; 'auto': DistNTT.auto_pieces, >= 2^22 "
+                         "elements per piece)")
+    ap.add_argument("--col-pieces", default=None,
                     help="four-step: column pieces whose transforms start as their part of the all-to-all "
-                         "arrives (default: as --pieces' default)")
+                         "arrives (default 1; 'auto')")
+    ap.add_argument("--no-parity", action="store_true", help="skip the post-timing parity check")
     ap.add_argument("--independent", action="store_true",
                     help="N > 1: one independent transform per rank (weak scaling, no data-path collective)")
     ap.add_argument("--cpu-log-n", type=int, default=22, help="C-oracle single-core sample size (log2)")
@@ -163,28 +173,177 @@ def load_traffic(tag: str):
     return ent.get("launch_bytes"), ent.get("profile")
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(args) -> int:
+    """``python bench.py --gpus N`` with no launcher: start the N ranks as children through
+    torch.distributed.run (one process per GPU), before this process makes any GPU call, and return
+    their exit status.  rank 0's JSON line reaches our stdout through the inherited file descriptor."""
+    import subprocess
+    import torch  # device_count() does not initialise the GPU on this image
+    rehearsal = os.environ.get("NTT_BENCH_EXCHANGE", "") == "host"
+    visible = torch.cuda.device_count()
+    if args.gpus > visible and not rehearsal:
+        print(f"bench.py: --gpus {args.gpus} but only {visible} visible device(s); refusing to run "
+              f"{args.gpus} ranks on fewer GPUs (NTT_BENCH_EXCHANGE=host rehearses them on one GPU)",
+              file=sys.stderr, flush=True)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__),
+           *sys.argv[1:]]
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "16"))
+    return subprocess.run(cmd, env=env).returncode
+
+
+def _kat_check(field_id: int, log_n: int, limbs: int, values, ks) -> bool:
+    """Closed-form KAT of x_j = j (any field; the reference's own input, GZKP-NTT.cu:1587):
+    X_0 = n (n - 1) / 2 and X_k = n / (w^k - 1) for k != 0, at the sampled k."""
+    from ntt_amd.fields import field_params
+    p, g = field_params(field_id)
+    n = 1 << log_n
+    w = pow(g, (p - 1) // n, p)
+    for k, v in zip(ks, values):
+        want = (n * (n - 1) // 2) % p if k == 0 else n * pow((pow(w, k, p) - 1) % p, p - 2, p) % p
+        if v != want:
+            return False
+    return True
+
+
+def _to_ints(rows):
+    """[k, limbs] int64 host rows (or [k] for one limb) -> Python ints."""
+    import numpy as np
+    a = rows.cpu().numpy()
+    if a.ndim == 1:
+        return [int(v) for v in a]
+    u = a.view(np.uint64)
+    return [sum(int(u[i, j]) << (64 * j) for j in range(u.shape[1])) for i in range(u.shape[0])]
+
+
+def _sample_ks(n: int):
+    import random
+    rng = random.Random(1234)
+    return sorted({0, 1, 2, n // 2, n - 1} | {rng.randrange(n) for _ in range(59)})
+
+
+def assemble_columns(parts, n1: int, c: int):
+    """Column-layout shares -> the natural-order vector: rank g holds [n1][c] with element (k1, kc) =
+    X[g c + kc + n2 k1] (n2 = G c), so [G][n1][c] transposed to [n1][G][c] is X in order."""
+    import torch
+    st = torch.stack(parts)
+    tail = tuple(st.shape[2:])
+    st = st.reshape((len(parts), n1, c) + tail).transpose(0, 1).contiguous()
+    return st.reshape((n1 * len(parts) * c,) + tail)
+
+
+def parity_four_step(args, eng, dist, rehearsal, local):
+    """After the timed region: forward of SURVEY §8d vector B (seed 2) through the distributed
+    schedule, gathered to rank 0 and compared with a one-GPU plan there (all n outputs), plus the
+    KAT of x_j = j at sampled k.  Returns the parity dict on rank 0 (None elsewhere)."""
+    import torch
+    from ntt_amd.ntt import NTTPlan
+    L = eng.layout
+    world, rank = L.world, L.rank
+
+    def gather_cols(t):
+        if rehearsal:  # gloo: CPU tensors
+            parts = [torch.empty_like(t, device="cpu") for _ in range(world)]
+            dist.all_gather(parts, t.cpu())
+            parts = [q.to(t.device) for q in parts]
+        else:
+            parts = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(parts, t)
+        return assemble_columns(parts, L.n1, L.c)
+
+    out = {}
+    x = eng.empty()
+    eng.fill(x, "random", seed=2)
+    eng.forward(x)
+    got = gather_cols(x)
+    xi = eng.empty()
+    eng.fill(xi, "iota", seed=0)
+    eng.forward(xi)
+    got_iota = gather_cols(xi)
+    torch.cuda.synchronize()
+    if rank == 0:
+        ref = NTTPlan(field_id=args.field, log_n=args.log_n, limbs64=args.limbs, device=local)
+        y = ref.empty()
+        ref.fill(y, "random", seed=2)
+        ref.forward(y)
+        torch.cuda.synchronize()
+        full_ok = torch.equal(got, y)
+        ks = _sample_ks(L.n)
+        idx = torch.tensor(ks, dtype=torch.int64, device=got_iota.device)
+        kat_ok = _kat_check(args.field, args.log_n, args.limbs, _to_ints(got_iota[idx]), ks)
+        out = {"status": "ok" if (full_ok and kat_ok) else "MISMATCH",
+               "full_vs_one_gpu_plan": full_ok, "kat_iota_sampled": kat_ok,
+               "checked": f"all 2^{args.log_n} forward outputs of vector B (seed 2), gathered from {world} "
+                          f"rank(s) to rank 0, against a one-GPU plan on rank 0; x_j = j against the "
+                          f"closed-form KAT at {len(ks)} sampled k"}
+        del ref, y
+    del got, got_iota, x, xi
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    return out if rank == 0 else None
+
+
+def parity_single(args, plan):
+    """After the timed region (N = 1 / independent ranks): x_j = j through the same plan, against the
+    closed-form KAT at sampled k, and forward + inverse of vector B returning the input."""
+    import torch
+    if args.inverse:
+        return {"status": "skipped", "reason": "parity is checked on the forward transform"}
+    x = plan.empty()
+    plan.fill(x, "iota", seed=0)
+    plan.forward(x)
+    ks = _sample_ks(plan.n)
+    idx = torch.tensor(ks, dtype=torch.int64, device=x.device)
+    kat_ok = _kat_check(args.field, args.log_n, args.limbs, _to_ints(x[idx]), ks)
+    y = plan.empty()
+    plan.fill(y, "random", seed=2)
+    y0 = y.clone()
+    plan.forward(y)
+    plan.inverse(y)
+    torch.cuda.synchronize()
+    rt_ok = torch.equal(y, y0)
+    return {"status": "ok" if (kat_ok and rt_ok) else "MISMATCH", "kat_iota_sampled": kat_ok,
+            "round_trip_vector_b": rt_ok,
+            "checked": f"x_j = j against the closed-form KAT at {len(ks)} sampled k; inverse(forward(B)) == B"}
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
+    if args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.independent and args.four_step:
         raise SystemExit("--independent and --four-step are exclusive")
     four_step = args.four_step or (world > 1 and not args.independent)
+    # NTT_BENCH_EXCHANGE=host: rehearsal of N ranks on ONE GPU (RCCL refuses duplicate devices): the
+    # all-to-all is staged through host memory over gloo.  Not a measurement of the product path.
+    rehearsal = os.environ.get("NTT_BENCH_EXCHANGE", "") == "host"
+    ndev = max(1, torch.cuda.device_count())
+    if world > ndev and not rehearsal:
+        raise SystemExit(f"{world} ranks but {ndev} visible device(s): one rank per GPU")
     # one rank per GPU; the modulo only matters when rehearsing several ranks on one device
-    local = local % max(1, torch.cuda.device_count())
+    local = local % ndev
     torch.cuda.set_device(local)
     n = 1 << args.log_n
 
     use_dist = world > 1 or four_step
-    # NTT_BENCH_EXCHANGE=host: rehearsal of N ranks on ONE GPU (RCCL refuses duplicate devices): the
-    # all-to-all is staged through host memory over gloo.  Not a measurement of the product path.
-    rehearsal = os.environ.get("NTT_BENCH_EXCHANGE", "") == "host"
+    rccl = False
     if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29512")
@@ -192,6 +351,7 @@ def main():
         os.environ.setdefault("WORLD_SIZE", "1")
         if four_step and not rehearsal:  # the data path exchanges over RCCL (all-to-all)
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+            rccl = True
         else:  # independent transforms (or the rehearsal): barrier / max / host exchange over gloo
             dist.init_process_group("gloo")
     if four_step:
@@ -235,7 +395,7 @@ def main():
 
     elapsed = t1 - t0
     if use_dist:
-        dev = f"cuda:{local}" if (four_step and not rehearsal) else "cpu"
+        dev = f"cuda:{local}" if rccl else "cpu"
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
@@ -266,8 +426,8 @@ def main():
                                f"{FIELD_NAMES[args.field]}, {args.limbs}x64-bit limbs, natural order, in place",
                    "log_n": args.log_n, "field": FIELD_NAMES[args.field], "limbs64": args.limbs,
                    "passes_log_radix": passes,
-                   "parallelism": ((f"REHEARSAL: four-step over {world} ranks, host-staged gloo exchange"
-                                    if rehearsal else
+                   "parallelism": ((f"REHEARSAL: four-step over {world} ranks on {ndev} GPU(s), host-staged "
+                                    f"gloo exchange" if rehearsal else
                                     f"four-step over {world} GPU(s) (RCCL all-to-all, one transform)") if four_step
                                    else ("single GPU" if world == 1 else
                                          f"{world} GPUs, one independent transform per rank (no data-path "
@@ -275,15 +435,25 @@ def main():
                    "transforms_per_step": jobs,
                    **({"exchange_pieces": len(eng.fs.pieces), "exchange_col_pieces": eng.fs.cp,
                        "split_log_n1_n2": [eng.layout.log_n1, eng.layout.log_n2]} if four_step else {})},
+        # world size of the RCCL (nccl-backend) process group carrying the data path; 0 = none
+        "rccl_ranks": world if rccl else 0,
     }
     if four_step:
         # rank 0's all-to-all window per transform (HIP events on the compute stream around the
-        # exchange: from the first piece's start to the last piece's arrival)
+        # exchange: from the first piece's start to the last piece's arrival; with the default single
+        # whole-block exchange it is the all-to-all alone).  Each rank sends every peer one block of
+        # r c elements per exchange over that pair's link, so the per-link rate is block / window.
         out["exchange_ms"] = exchange_ms
+        peer_bytes = eng.layout.chunk * elem_bytes
+        out["exchange_bytes_per_peer"] = peer_bytes
+        out["exchange_gbps_per_link"] = (peer_bytes / (exchange_ms * 1e-3) / 1e9
+                                         if exchange_ms and world > 1 else None)
+        if rehearsal:
+            out["exchange_note"] = "host-staged gloo exchange on one GPU: not an xGMI link rate"
     # ---- SURVEY §8(d) roofline of the whole transform: 2 n S algorithmic bytes per transform
     gpus_per_transform = world if four_step else 1
     alg_transform = 2 * n * elem_bytes
-    t_transform = ms_per_step * 1e-3 * (1 if four_step else 1)  # every rank runs its transform(s) per step
+    t_transform = ms_per_step * 1e-3  # every rank runs its transform(s) per step
     achieved = alg_transform / t_transform / gpus_per_transform / 1e9
     tag = f"f{args.field}_L{args.limbs}_n{args.log_n}_w{gpus_per_transform}{'_inv' if args.inverse else ''}"
     launch_bytes, prof_src = load_traffic(tag) if not four_step else (None, "four-step: not profiled")
@@ -318,6 +488,14 @@ def main():
                                     "unit": "T lane-MAD/s", "frac": ach / MAD_PEAK_T,
                                     "mads_per_launch": mads, "kernel": f"launch {k} of {len(launch_avg)}"}
     out["roofline"] = roof
+    # ---- parity, outside the timed region
+    if not args.no_parity:
+        if four_step:
+            par = parity_four_step(args, eng, dist, rehearsal, local)
+        else:
+            par = parity_single(args, plan) if rank == 0 else None
+        if rank == 0:
+            out["parity"] = par
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args.field, args.limbs if args.limbs != 1 else 1, args.cpu_log_n)
@@ -327,6 +505,8 @@ def main():
         print(json.dumps(out), flush=True)
     if use_dist:
         dist.destroy_process_group()
+    if rank == 0 and isinstance(out.get("parity"), dict) and out["parity"].get("status") == "MISMATCH":
+        sys.exit(3)
 
 
 if __name__ == "__main__":

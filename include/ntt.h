@@ -44,6 +44,12 @@ extern "C" {
 #define NTT_ERR_RCCL (-3)     /* RCCL error (multi-GPU) */
 #define NTT_ERR_FIELD (-4)    /* modulus unsupported (even, too large, no root of unity of order n) */
 #define NTT_ERR_NODEV (-5)    /* no HIP device */
+#define NTT_ERR_DEVICE (-6)   /* an inter-workgroup wait of an earlier call on this plan gave up at its
+                               * watchdog (in-place or single-launch schedules; never expected): that
+                               * call's output is wrong.  Every call on the plan returns this until
+                               * ntt_plan_device_status clears the report.  The blocking shims return it
+                               * for the call itself (and clear it).  The reference asserts instead
+                               * (GZKP-NTT.cu:1527). */
 
 /* field ids */
 #define NTT_FIELD_P469762049 0   /* 7*2^26+1, generator 3 (GZKP-NTT.cu:7-8) */
@@ -106,9 +112,11 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
  * ntt_plan_device_status reports a wait that gave up (a watchdog; never expected). */
 #define NTT_PLAN_SINGLE_LAUNCH 32u
 int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags);
-/* Device-side status of a plan since the last call (blocking; clears it).  *bad bit 0: an
- * inter-workgroup wait gave up at its watchdog (NTT_PLAN_SINGLE_LAUNCH, or the fused digit reversal
- * of NTT_PLAN_IN_PLACE): that call's output is wrong.  The checked build (ntt_amd/libntt_debug.so,
+/* Device-side status of a plan (blocking: synchronises the device, then reads and clears it).
+ * *bad bit 0: an inter-workgroup wait gave up at its watchdog (NTT_PLAN_SINGLE_LAUNCH, or the fused
+ * digit reversal of NTT_PLAN_IN_PLACE): that call's output is wrong (the workgroup that gave up
+ * skipped its stores), and until this call clears the report every other call on the plan returns
+ * NTT_ERR_DEVICE.  The checked build (ntt_amd/libntt_debug.so,
  * same ABI, `python -m ntt_amd.build --debug`) adds, from checks inside every pass kernel:
  *   0x100  an element index outside its buffer (the access went to element 0 instead)
  *   0x200  a caller input element >= p (the inputs must be canonical, as in the reference)
@@ -116,6 +124,10 @@ int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned li
  *   0x800  an output element >= p
  * The product build never sets these bits. */
 int ntt_plan_device_status(ntt_plan* plan, unsigned* bad);
+/* Poll limit of the plan's bounded inter-workgroup waits (default 2^21, about 2 s; read at each
+ * launch).  0 makes every wait that is not already satisfied give up at once: a test hook for the
+ * NTT_ERR_DEVICE path (tests/test_gpu_watchdog.py). */
+int ntt_plan_set_watchdog(ntt_plan* plan, unsigned spins);
 
 /* Modulus-generic plan, like big-num.cu's `prime` / `omega` kernel arguments (big-num.cu:68,173,260):
  * modulus and generator given as limbs64 little-endian 64-bit limbs. */
@@ -315,8 +327,8 @@ int ntt_mplan_info(const ntt_mplan* plan, uint64_t* local_n, unsigned* log_n1, u
  * <= c; the ntt_rplan_*_piece layouts): row piece i's exchange (grouped ncclSend / ncclRecv on a
  * per-device communication stream) overlaps the row transforms of piece i + 1, the last row piece
  * goes out per column piece and each column piece's transforms start when it has arrived (the
- * inverse mirrors it).  Default: row pieces of >= 2^22 elements, column pieces of >= 2^21, at most 4
- * (2^24 over 2 GPUs: 2 x 4; over 8: 1 x 1; 2^28 over 8: 8 x 4). */
+ * inverse mirrors it).  Default: 1 x 1, one whole-block exchange per transform (the pieces have
+ * not yet measured a gain). */
 int ntt_mplan_set_pieces2(ntt_mplan* plan, unsigned row_pieces, unsigned col_pieces);
 /* Row pieces only (1..16, <= r; rounded down to a power of two), one column piece. */
 int ntt_mplan_set_pieces(ntt_mplan* plan, unsigned pieces);

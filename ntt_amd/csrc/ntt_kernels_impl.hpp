@@ -325,23 +325,42 @@ __device__ __forceinline__ void ipn_signal_read(const PassArgs<E>& A, uint32_t m
   if (threadIdx.x == 0 && __hip_atomic_fetch_add(line, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == A.ipn_strips - 1)
     __hip_atomic_store(line + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-template <class E>
-__device__ __forceinline__ void ipn_wait_mirror(const PassArgs<E>& A, uint32_t midrev) {
-  if (threadIdx.x == 0) {
-    // relaxed global loads of the ready word (no read-modify-write polls: DESIGN §4)
-    typedef __attribute__((address_space(1))) uint32_t gu32;
-    gu32* const ready = (gu32*)(A.ipn_sync + 32 * (1 + midrev) + 1);
-    for (uint32_t spins = 0;; ++spins) {
-      if (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-      if (spins < 8) __builtin_amdgcn_s_sleep(4);
-      else __builtin_amdgcn_s_sleep(32);
-      if (spins == (1u << 21)) {  // ~2 s: give up (watchdog word; the output is then wrong)
-        __hip_atomic_store(A.ipn_sync + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
+// A wait gave up (Watchdog, ntt_kernels.hpp): the launch's abort word, then the plan's host-mapped
+// report word (system scope: the host reads it at the plan's next call without a device query).
+__device__ __forceinline__ void watchdog_trip(uint32_t* abort_w, const Watchdog& wd) {
+  __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (wd.report) __hip_atomic_store(wd.report, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// One lane's bounded poll of `word` with relaxed agent-scope global loads (no read-modify-write
+// polls: DESIGN §4), sleeping S0 below N0 polls, S1 below N1, S2 after.  True once the word is
+// non-zero; false when the wait gave up: wd.spins polls without it (this lane trips the watchdog) or
+// another workgroup of the launch gave up first (its abort word is set).
+template <int S0, uint32_t N0, int S1, uint32_t N1, int S2>
+__device__ __forceinline__ bool poll_bounded(uint32_t* word, uint32_t* abort_w, const Watchdog& wd) {
+  typedef __attribute__((address_space(1))) uint32_t gu32;  // a global (not flat) access
+  gu32* const g = (gu32*)word;
+  gu32* const ab = (gu32*)abort_w;
+  for (uint32_t spins = 0;; ++spins) {
+    if (__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return true;
+    if (spins >= wd.spins) {
+      watchdog_trip(abort_w, wd);
+      return false;
     }
+    if (spins >= 16 && __hip_atomic_load(ab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    if (spins < N0) __builtin_amdgcn_s_sleep(S0);
+    else if (spins < N1) __builtin_amdgcn_s_sleep(S1);
+    else __builtin_amdgcn_s_sleep(S2);
   }
+}
+// True (workgroup-uniform) once slab midrev has been read; false when the wait gave up, and the tile
+// must then not store: its outputs would overwrite elements of midrev that are still unread.
+template <class E>
+__device__ __forceinline__ bool ipn_wait_mirror(const PassArgs<E>& A, uint32_t midrev) {
+  __shared__ uint32_t s_ok;
+  if (threadIdx.x == 0)
+    s_ok = poll_bounded<4, 8, 32, 8, 32>(A.ipn_sync + 32 * (1 + midrev) + 1, A.ipn_sync + 2, A.wd) ? 1u : 0u;
   __syncthreads();
+  return s_ok != 0u;
 }
 
 // LDS of one pass tile (words), and whether the pass stages its w_R^e table in LDS: E::LDS_TW
@@ -590,7 +609,9 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
   static_assert(S::nsub <= 6, "sub-stages");
 
   // ------------------------------------------------------------------ output
-  if constexpr (IPN) ipn_wait_mirror(A, midrev);  // the slab this tile writes into has been read
+  if constexpr (IPN) {  // the slab this tile writes into has been read (or the wait gave up: no stores)
+    if (!ipn_wait_mirror(A, midrev)) return;
+  }
 #if NTT_PRIO & 2
   __builtin_amdgcn_s_setprio(1);  // timing experiment: finishing tiles drain first
 #endif
@@ -745,7 +766,7 @@ void k_final_ipn(uint32_t* data, const PassArgs<E> A) {
       A.ipn_sync[32 * (1 + m)] = 0u;
       A.ipn_sync[32 * (1 + m) + 1] = 0u;
     }
-    if (t == 0) A.ipn_sync[0] = A.ipn_sync[1] = 0u;
+    if (t == 0) A.ipn_sync[0] = A.ipn_sync[1] = A.ipn_sync[2] = 0u;
   }
 }
 
@@ -773,6 +794,34 @@ hipError_t launch_final_ipn(int logr, uint32_t* data, const PassArgs<E>& A, uint
   }
 }
 
+// Workgroups of k_final_ipn<E, logr> the device keeps resident at once (occupancy x CUs; 0 if the
+// query fails or the radix has no instance)
+template <class E>
+uint32_t launch_final_ipn_capacity(int logr, int device) {
+  constexpr int TL = tile_log_of<E>();
+  constexpr int NT = (1 << TL) / E::EPT;
+  int cus = 0, per = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
+  hipError_t e = hipErrorInvalidValue;
+  switch (logr) {
+#define NTT_IPN_OCC(R)                                                                                   \
+  case R:                                                                                                \
+    if constexpr (R <= TL - E::MIN_COLS_LOG)                                                             \
+      e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_final_ipn<E, R>), NT, 0); \
+    break;
+    NTT_IPN_OCC(3)
+    NTT_IPN_OCC(4)
+    NTT_IPN_OCC(5)
+    NTT_IPN_OCC(6)
+    NTT_IPN_OCC(7)
+    NTT_IPN_OCC(8)
+    NTT_IPN_OCC(9)
+#undef NTT_IPN_OCC
+    default: break;
+  }
+  return (e == hipSuccess && per > 0 && cus > 0) ? (uint32_t)per * (uint32_t)cus : 0u;
+}
+
 // ---------------------------------------------------------------------------- fused 3-pass launch
 // BASELINE config 2 asks for the 2^20 transform as a single kernel (the reference's SSIP schedule is
 // 4 launches at 2^20, GZKP-NTT.cu:1509-1545).  k_fused3 runs the three passes of a 3-pass schedule in
@@ -790,8 +839,9 @@ hipError_t launch_final_ipn(int logr, uint32_t* data, const PassArgs<E>& A, uint
 // (sc1), every wave drains them (s_waitcnt vmcnt(0)), a workgroup barrier, then one lane's agent-scope
 // counter add; the group's last arrival raises a ready word; the consumer polls it, takes ONE
 // agent-scope acquire, waits, barrier, plain loads.
-// Every dependency wait is bounded (watchdog word, then the tile runs anyway: wrong output, no hang),
-// so every wave reaches the exit; the last workgroup out re-zeroes the counters for the next launch.
+// Every dependency wait is bounded (Watchdog: a workgroup whose wait gives up runs no further tile,
+// the launch's other waits give up at once, and the plan's next call returns NTT_ERR_DEVICE), so every
+// wave reaches the exit; the last workgroup out re-zeroes the counters for the next launch.
 // Producer: every wave drains its write-through stores, a barrier, then one lane counts the tile in;
 // the group's last arrival (told by the value its add returns) raises the group's ready word, which
 // lies on a 128-B line of its own.  Consumers poll only that word: 128 pollers on the counter itself
@@ -805,26 +855,18 @@ __device__ __forceinline__ void fused_publish(uint32_t* cnt, uint32_t* ready, ui
 // Consumer: one lane polls the ready word with relaxed agent-scope loads (compare-exchange polls,
 // read-modify-writes at the memory side, queued the producers' updates behind them: 2^20 single
 // launch 0.162 -> see DESIGN §4), sleeping 60 ns .. 1 us between polls; then ONE agent-scope acquire, its wait, and
-// the workgroup barrier before any load of the handed-off tile.  Bounded: after ~2 s it gives up and
-// raises the watchdog word (the output is then wrong; every wave still reaches the exit).
-__device__ __forceinline__ void fused_wait(uint32_t* ready, uint32_t* watchdog, uint32_t dbg) {
-  if (dbg & 1u) return;  // diagnostics only: no dependency waits (wrong output)
+// the workgroup barrier before any load of the handed-off tile.  Bounded (Watchdog): false
+// (workgroup-uniform) when the wait gave up; the workgroup then runs no further tile.
+__device__ __forceinline__ bool fused_wait(uint32_t* ready, const FusedArgs& F) {
+  if (F.dbg & 1u) return true;  // diagnostics only: no dependency waits (wrong output)
+  __shared__ uint32_t s_ok;
   if (threadIdx.x == 0) {
-    typedef __attribute__((address_space(1))) uint32_t gu32;  // a global (not flat) access
-    gu32* const g = (gu32*)ready;
-    for (uint32_t spins = 0; __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;) {
-      if (spins < 4) __builtin_amdgcn_s_sleep(2);
-      else if (spins < 16) __builtin_amdgcn_s_sleep(8);
-      else __builtin_amdgcn_s_sleep(32);
-      if (++spins == (1u << 21)) {
-        __hip_atomic_store(watchdog, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
+    s_ok = poll_bounded<2, 4, 8, 16, 32>(ready, F.sync + 2, F.wd) ? 1u : 0u;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  return s_ok != 0u;
 }
 
 template <class E>
@@ -891,7 +933,10 @@ void k_fused3(const FusedKArgs<E> K) {
   }
   while (tk < 2 * F.tiles) {  // pass 2: scratch in place (Shoup-pair outer twiddles)
     const uint32_t w = tk - F.tiles, g = w & ((1u << F.cg_log) - 1);
-    fused_wait(F.sync + F.rbase + 32 * (g >> F.k2_shift), F.sync + 2, F.dbg);
+    if (!fused_wait(F.sync + F.rbase + 32 * (g >> F.k2_shift), F)) {
+      tk = total;  // gave up (watchdog): no further tile, straight to the exit
+      break;
+    }
     const FusedKArgs<E>& L = fused_kargs<E>();
     pass_tile<E, R2, KIND_COLUMN, true, true, PRO_NONE, true, 0, true, true, true>(L.scratch, L.scratch, L.A2, w, 0,
                                                                                      lds, lds_tw);
@@ -902,7 +947,7 @@ void k_fused3(const FusedKArgs<E> K) {
   }
   while (tk < total) {  // final pass: scratch -> the caller's buffer, natural order
     const uint32_t w = tk - 2 * F.tiles;
-    fused_wait(F.sync + F.rbase + 32 * (F.n12 + (w >> F.r2)), F.sync + 2, F.dbg);
+    if (!fused_wait(F.sync + F.rbase + 32 * (F.n12 + (w >> F.r2)), F)) break;
     const FusedKArgs<E>& L = fused_kargs<E>();
     pass_tile<E, R3, KIND_FINAL, false, true, PRO_NONE, true, 0, false, false, true>(L.scratch, L.dst, L.A3, w, 0,
                                                                                        lds, lds_tw);
@@ -911,8 +956,7 @@ void k_fused3(const FusedKArgs<E> K) {
   if (t == 0 && __hip_atomic_fetch_add(F.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == F.nwg - 1) {
     // the last workgroup out: nobody touches the counters again in this launch
     const uint32_t words = F.rbase + 32 * (F.n12 + F.n23);
-    for (uint32_t i = 0; i < words; ++i)
-      if (i != 2) __hip_atomic_store(F.sync + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t i = 0; i < words; ++i) __hip_atomic_store(F.sync + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -929,28 +973,22 @@ void k_fused3(const FusedKArgs<E> K) {
 // workgroups made each barrier cost ~0.15 ms.
 // The arrival counter is cumulative (barrier k completes at k G arrivals); the last workgroup out
 // re-zeroes the words for the next launch.
-__device__ __forceinline__ void fused_grid_barrier(const FusedArgs& F, uint32_t k) {
+// False (workgroup-uniform) when the wait gave up (Watchdog): the workgroup then skips the passes left.
+__device__ __forceinline__ bool fused_grid_barrier(const FusedArgs& F, uint32_t k) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores are done
   __syncthreads();
+  __shared__ uint32_t s_ok;
   uint32_t* const go = F.sync + F.rbase + 32 * (k - 1);
   if (threadIdx.x == 0) {
     if (__hip_atomic_fetch_add(F.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k * gridDim.x - 1)
       __hip_atomic_store(go, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // poll the go word with relaxed agent-scope loads (global, not flat), bounded like fused_wait
-    typedef __attribute__((address_space(1))) uint32_t gu32;
-    gu32* const g = (gu32*)go;
-    for (uint32_t spins = 0; __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;) {
-      if (spins < 16) __builtin_amdgcn_s_sleep(4);
-      else __builtin_amdgcn_s_sleep(32);
-      if (++spins == (1u << 21)) {
-        __hip_atomic_store(F.sync + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
+    s_ok = poll_bounded<4, 16, 32, 16, 32>(go, F.sync + 2, F.wd) ? 1u : 0u;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  return s_ok != 0u;
 }
 
 template <class E, int R1, int R2, int R3>
@@ -969,15 +1007,15 @@ void k_fused3b(const FusedKArgs<E> K) {
                                                                                                 w, 0, lds, lds_tw);
     __syncthreads();  // every wave is done with this tile's LDS
   }
-  fused_grid_barrier(F, 1);
-  for (uint32_t w = blockIdx.x; w < F.tiles; w += G) {  // pass 2: scratch in place
+  bool ok = fused_grid_barrier(F, 1);
+  for (uint32_t w = blockIdx.x; ok && w < F.tiles; w += G) {  // pass 2: scratch in place
     const FusedKArgs<E>& L = fused_kargs<E>();
     pass_tile<E, R2, KIND_COLUMN, true, true, PRO_NONE, true, 0, true, true, true>(L.scratch, L.scratch, L.A2,
                                                                                                w, 0, lds, lds_tw);
     __syncthreads();
   }
-  fused_grid_barrier(F, 2);
-  for (uint32_t w = blockIdx.x; w < F.tiles; w += G) {  // final pass: scratch -> the caller's buffer
+  ok = ok && fused_grid_barrier(F, 2);  // a workgroup that gave up does not arrive: the others give up too
+  for (uint32_t w = blockIdx.x; ok && w < F.tiles; w += G) {  // final pass: scratch -> the caller's buffer
     const FusedKArgs<E>& L = fused_kargs<E>();
     pass_tile<E, R3, KIND_FINAL, false, true, PRO_NONE, true, 0, false, false, true>(L.scratch, L.dst, L.A3, w, 0,
                                                                                        lds, lds_tw);
@@ -987,6 +1025,7 @@ void k_fused3b(const FusedKArgs<E> K) {
     // the last workgroup out: every other one has passed both barriers
     __hip_atomic_store(F.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(F.sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(F.sync + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(F.sync + F.rbase, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(F.sync + F.rbase + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -1764,6 +1803,7 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
                                           hipStream_t);                                                            \
   template hipError_t launch_digitrev_swap<E>(uint32_t*, const DrevArgs&, uint32_t, hipStream_t);                  \
   template hipError_t launch_final_ipn<E>(int, uint32_t*, const PassArgs<E>&, uint32_t, hipStream_t);              \
+  template uint32_t launch_final_ipn_capacity<E>(int, int);                                                        \
   template hipError_t launch_pointwise<E>(const uint32_t*, const uint32_t*, uint32_t*, size_t,                     \
                                           const typename E::Args&, const uint32_t*, hipStream_t, const FsMap*);    \
   template hipError_t launch_build_tw<E>(uint32_t*, size_t, uint32_t, uint32_t, uint32_t, const uint32_t*,        \

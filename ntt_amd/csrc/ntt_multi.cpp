@@ -17,8 +17,8 @@
 // Forward: row piece i is exchanged (grouped ncclSend / ncclRecv on a per-device communication
 // stream, ordered by events) while the row transforms of piece i + 1 run; the last row piece goes out
 // column piece by column piece, and the column transforms of piece k start when its unit has arrived.
-// The inverse mirrors it.  Row pieces keep >= 2^22 elements, column pieces >= 2^21 (at most 4);
-// ntt_mplan_set_pieces / ntt_mplan_set_pieces2 override.
+// The inverse mirrors it.  Default 1 x 1 (one whole-block exchange); ntt_mplan_set_pieces /
+// ntt_mplan_set_pieces2 select pieces.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -185,9 +185,10 @@ int exchange(ntt_mplan* m, const std::vector<void*>& send, const std::vector<voi
   return (st == ncclSuccess && end == ncclSuccess) ? NTT_OK : abort_comms(m);
 }
 
-size_t chunk_words(const ntt_mplan* m) {  // per-peer chunk of one vector: r * c elements
-  return (1ull << (m->log_r + m->log_c)) * (m->elem_bytes / 8);
+size_t peer_elems(const ntt_mplan* m) {  // per-peer chunk of one vector: r * c = local_n / G elements
+  return 1ull << (m->log_r + m->log_c);
 }
+size_t chunk_words(const ntt_mplan* m) { return peer_elems(m) * (m->elem_bytes / 8); }
 
 // Runs of every peer block (blocks of peer_elems elements; runs (offset, length) in elements) as
 // grouped ncclSend / ncclRecv on the communication streams.
@@ -295,8 +296,9 @@ int forward_vectors(ntt_mplan* m, void* const* const* v, int nv, void* const* st
   } else {
     // row piece i's exchange overlaps the row transforms of piece i + 1; the last row piece goes out
     // per column piece, whose column transforms start as soon as that unit has arrived
+    // one peer block = the nv vectors' r x c chunks ([G][nv][r c] send / receive buffers)
     const unsigned P = m->pieces, Q = m->col_pieces;
-    const size_t c = 1ull << m->log_c, ra = (1ull << m->log_r) / P, cm = c / Q, peer = nv * m->local_n();
+    const size_t c = 1ull << m->log_c, ra = (1ull << m->log_r) / P, cm = c / Q, peer = nv * peer_elems(m);
     for (unsigned i = 0; i < P; ++i) {
       for (int g = 0; g < m->ngpus; ++g)
         for (int k = 0; k < nv; ++k)
@@ -347,7 +349,7 @@ int inverse_vector(ntt_mplan* m, void* const* a, void* const* b, void* const* ou
   }
   // column piece q's exchange overlaps the column transforms of piece q + 1; the last column piece
   // goes out per row piece, whose inverse row transforms start as soon as that unit has arrived
-  const size_t r = 1ull << m->log_r, ra = r / P, cm = (1ull << m->log_c) / Q, peer = m->local_n();
+  const size_t r = 1ull << m->log_r, ra = r / P, cm = (1ull << m->log_c) / Q, peer = peer_elems(m);
   for (unsigned q = 0; q < Q; ++q) {
     for (int g = 0; g < m->ngpus; ++g)
       if (int rc = ntt_rplan_inverse_cols_piece(m->rp[g], a[g], b ? b[g] : nullptr, m->send[g], q, P, Q,
@@ -421,12 +423,10 @@ int ntt_mplan_create(ntt_mplan** out, int field_id, unsigned log_n, unsigned lim
         if (hipEventCreateWithFlags(&m->ev_done[g * ntt_mplan::kMaxPieces + i], hipEventDisableTiming) != hipSuccess)
           rc = NTT_ERR_HIP;
     }
-    // row pieces of >= 2^22 elements, column pieces of >= 2^21 (at most 4): DistNTT.auto_pieces
-    const size_t local = m->local_n();
-    while (m->pieces < 8 && (local >> 1) / m->pieces >= (size_t(1) << 22)) m->pieces *= 2;
-    while (m->col_pieces < 4 && (local >> 1) / m->col_pieces >= (size_t(1) << 21)) m->col_pieces *= 2;
-    if (m->pieces > (1u << m->log_r)) m->pieces = 1u << m->log_r;
-    if (m->col_pieces > (1u << m->log_c)) m->col_pieces = 1u << m->log_c;
+    // one whole-block exchange per transform by default (DistNTT.auto_pieces): the pipelined pieces
+    // never measured a gain on one GPU and their timings varied run to run, so they
+    // are opt-in (ntt_mplan_set_pieces2) until a multi-GPU node shows that they win
+    m->pieces = m->col_pieces = 1;
   }
   if (rc != NTT_OK) {
     delete m;

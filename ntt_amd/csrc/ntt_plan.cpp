@@ -114,6 +114,26 @@ struct PlanBase {
   bool profiling = false;
   hipEvent_t ev[kSlots][kEv] = {};
   unsigned ev_used = 0, slot = 0, nrec = 0;
+  // Watchdog report (ntt_kernels.hpp): a host-mapped word that a kernel sets when one of its bounded
+  // inter-workgroup waits gives up.  Every later call on the plan returns NTT_ERR_DEVICE (a plain host
+  // read, no device query) until ntt_plan_device_status reads and clears it.
+  uint32_t* h_watch = nullptr;  // host pointer (hipHostMalloc, mapped, coherent)
+  uint32_t* d_watch = nullptr;  // its device alias (the kernels' Watchdog::report)
+  uint32_t wd_spins = 1u << 21; // poll limit of a wait (~2 s); ntt_plan_set_watchdog
+  bool tripped() const { return h_watch && __atomic_load_n(h_watch, __ATOMIC_ACQUIRE) != 0u; }
+  void clear_trip() {
+    if (h_watch) __atomic_store_n(h_watch, 0u, __ATOMIC_RELEASE);
+  }
+  ntt::Watchdog watchdog() const { return ntt::Watchdog{d_watch, wd_spins}; }
+  int alloc_watch() {
+    if (hipHostMalloc(reinterpret_cast<void**>(&h_watch), 4, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+      h_watch = nullptr;
+      return NTT_ERR_HIP;
+    }
+    *h_watch = 0u;
+    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d_watch), h_watch, 0) != hipSuccess) return NTT_ERR_HIP;
+    return NTT_OK;
+  }
   void begin(hipStream_t st) {
     if (!profiling) return;
     slot = nrec % kSlots;
@@ -416,6 +436,7 @@ struct PlanImpl final : PlanBase {
     if (d_ipn) (void)hipFree(d_ipn);
     if (d_pw) (void)hipFree(d_pw);
     if (d_dbg) (void)hipFree(d_dbg);
+    if (h_watch) (void)hipHostFree(h_watch);
     for (auto& row : ev)
       for (auto& e : row)
         if (e) (void)hipEventDestroy(e);
@@ -591,6 +612,7 @@ struct PlanImpl final : PlanBase {
     if (hipMalloc(&d_tab, host.size() * 4) != hipSuccess ||
         hipMemcpy(d_tab, host.data(), host.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
       rc = NTT_ERR_HIP;
+    if (rc == NTT_OK) rc = alloc_watch();
 #if NTT_DEBUG_CHECKS
     // debug builds: the status word every kernel of this plan records check failures in
     if (rc == NTT_OK && (hipMalloc(&d_dbg, 4) != hipSuccess || hipMemset(d_dbg, 0, 4) != hipSuccess)) rc = NTT_ERR_HIP;
@@ -1088,7 +1110,9 @@ struct PlanImpl final : PlanBase {
       if constexpr (std::is_same_v<E, Eng256>) {  // the engine k_fused3 is instantiated for
         if (!io && !inplace && batch == 1 && fused_enabled() && fused_ready(PA)) {
           // one persistent launch for the three passes (NTT_PLAN_SINGLE_LAUNCH, k_fused3)
-          e = launch_fused3<E>((int)r[0], (int)r[1], (int)r[2], in, work, out, PA[0], PA[1], PA[2], fused_args(), st);
+          FusedArgs F = fused_args();
+          F.wd = watchdog();
+          e = launch_fused3<E>((int)r[0], (int)r[1], (int)r[2], in, work, out, PA[0], PA[1], PA[2], F, st);
           mark(st);
           return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
         }
@@ -1105,6 +1129,7 @@ struct PlanImpl final : PlanBase {
         B.ipn_sync = d_ipn;
         B.ipn_order = d_ipn + 32 * (1 + ipn_slabs);
         B.ipn_strips = ipn_strips;
+        B.wd = watchdog();
         e = launch_final_ipn<E>((int)r[npass - 1], out, B, grid, st);
         mark(st);
       } else if (e == hipSuccess) {
@@ -1198,16 +1223,13 @@ struct PlanImpl final : PlanBase {
     }
   }
   const FusedArgs& fused_args() const { return fargs; }
-  // watchdog of the fused schedule: non-zero when a dependency wait gave up (then cleared)
+  // bit 0: a bounded wait gave up (the watchdog report, PlanBase::h_watch); then cleared.  Blocking:
+  // the device is synchronised first, so the report covers every call enqueued before.
   int device_status(unsigned* bad) override {
     *bad = 0;
-    for (uint32_t* d : {d_sync, d_ipn}) {
-      if (!d) continue;
-      uint32_t w = 0;
-      if (hipMemcpy(&w, d + 2, 4, hipMemcpyDeviceToHost) != hipSuccess) return NTT_ERR_HIP;
-      if (w && hipMemset(d + 2, 0, 4) != hipSuccess) return NTT_ERR_HIP;
-      *bad |= w;
-    }
+    if (hipDeviceSynchronize() != hipSuccess) return NTT_ERR_HIP;
+    if (tripped()) *bad |= 1u;
+    clear_trip();
     if (d_dbg) {  // debug builds: NTT_DBG_* bits (engines.hpp)
       uint32_t w = 0;
       if (hipMemcpy(&w, d_dbg, 4, hipMemcpyDeviceToHost) != hipSuccess) return NTT_ERR_HIP;
@@ -1237,7 +1259,10 @@ struct PlanImpl final : PlanBase {
     const unsigned mid_log = log_n - r[0] - rp;
     ipn_slabs = 1u << mid_log;
     ipn_strips = 1u << (r[0] - (tl - rp));  // R_1 / T, T = TILE / R_p
-    if (r[0] < tl - rp || 2 * ipn_strips > 1024) return false;
+    // the deadlock-freedom argument of k_final_ipn needs a slab pair's tiles resident together: at
+    // most 128 per pair, and no more than the device keeps resident
+    if (r[0] < tl - rp || 2 * ipn_strips > 128) return false;
+    if (launch_final_ipn_capacity<E>((int)rp, device) < 2 * ipn_strips) return false;
     // slab order: m, then its mirror (the final pass's middle-digit reversal, as k_pass computes it)
     std::vector<uint32_t> order, seen(ipn_slabs, 0);
     auto rev = [&](uint32_t m) {
@@ -1520,10 +1545,13 @@ int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned li
 }
 
 // Every entry point that launches work runs it on the plan's device (saved and restored around
-// the call), so a caller whose current device differs still gets the right one.
+// the call), so a caller whose current device differs still gets the right one.  A plan whose
+// watchdog has tripped (PlanBase::h_watch) refuses work with NTT_ERR_DEVICE until
+// ntt_plan_device_status clears the report.
 extern "C++" template <class F>
-static int on_device(ntt_plan* plan, F&& f) {
+static int on_device(ntt_plan* plan, F&& f, bool check_watchdog = true) {
   if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
+  if (check_watchdog && plan->impl->tripped()) return set_err(NTT_ERR_DEVICE);
   int cur = 0;
   (void)hipGetDevice(&cur);
   if (cur != plan->impl->device) (void)hipSetDevice(plan->impl->device);
@@ -1566,7 +1594,13 @@ int ntt_count_noncanonical(ntt_plan* plan, const void* d, uint64_t count, uint64
 
 int ntt_plan_device_status(ntt_plan* plan, unsigned* bad) {
   if (!bad) return set_err(NTT_ERR_ARG);
-  return on_device(plan, [&](PlanBase& P) { return P.device_status(bad); });
+  return on_device(plan, [&](PlanBase& P) { return P.device_status(bad); }, false);
+}
+
+int ntt_plan_set_watchdog(ntt_plan* plan, unsigned spins) {
+  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
+  plan->impl->wd_spins = spins;
+  return set_err(NTT_OK);
 }
 
 int ntt_polymul(ntt_plan* plan, void* a, void* b, void* c, void* s) {
@@ -1675,6 +1709,9 @@ const char* ntt_strerror(int status) {
     case NTT_ERR_RCCL: return "RCCL error";
     case NTT_ERR_FIELD: return "unsupported modulus or no root of unity of this order";
     case NTT_ERR_NODEV: return "no HIP device";
+    case NTT_ERR_DEVICE:
+      return "an inter-workgroup wait of an earlier call gave up (watchdog): that call's output is wrong; "
+             "ntt_plan_device_status clears the report";
     default: return "unknown status";
   }
 }
@@ -1691,6 +1728,10 @@ struct CachedPlan {
   std::unique_ptr<ntt_plan> plan;
   std::mutex run_mu;
   uint64_t last_use = 0;
+  hipEvent_t done = nullptr;  // the blocking shims wait on this, like the reference's cudaEventSynchronize
+  ~CachedPlan() {
+    if (done) (void)hipEventDestroy(done);
+  }
 };
 }  // namespace
 static std::mutex g_cache_mu;
@@ -1743,11 +1784,24 @@ extern "C" void ntt_shim_cache_clear(void) {
   g_cache.clear();
 }
 
-// forward on the default stream, then wait for the device, under the plan's lock
+// Forward on the default stream, then wait for an event recorded after it (GZKP-NTT.cu:1547 waits on
+// its own event the same way), under the plan's lock: work the caller runs on other non-blocking
+// streams is not waited on.  A tripped watchdog (the plan's report, read after the wait) is this
+// call's error, and is cleared so that the cached plan serves the next call.
 static int blocking_forward(const std::shared_ptr<CachedPlan>& cp, void* d) {
   std::lock_guard<std::mutex> lk(cp->run_mu);
   int rc = ntt_forward(cp->plan.get(), d, nullptr);
-  if (rc == NTT_OK && hipDeviceSynchronize() != hipSuccess) rc = NTT_ERR_HIP;
+  if (rc == NTT_OK && !cp->done && hipEventCreateWithFlags(&cp->done, hipEventDisableTiming) != hipSuccess) {
+    cp->done = nullptr;
+    rc = NTT_ERR_HIP;
+  }
+  if (rc == NTT_OK && (hipEventRecord(cp->done, nullptr) != hipSuccess || hipEventSynchronize(cp->done) != hipSuccess))
+    rc = NTT_ERR_HIP;
+  PlanBase& P = *cp->plan->impl;
+  if (P.tripped()) {
+    P.clear_trip();
+    if (rc == NTT_OK) rc = NTT_ERR_DEVICE;
+  }
   return set_err(rc);
 }
 

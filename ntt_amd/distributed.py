@@ -325,19 +325,22 @@ class DistNTT:
     stream, overlapping the local transforms on both sides of the exchange (FourStep).
     """
 
-    # A piece's row transforms must still fill the GPU: every pass of a local transform launches one
-    # 1024-element workgroup tile per 1024 elements, and 256 CUs x 4 resident workgroups want several
-    # rounds of them.  Measured on one GPU (profiles/r02_pipe/, configs.jsonl): 2^28 over 8 virtual
-    # ranks (2^25 per rank) 34.5 -> 33.5 ms with 4 pieces; 2^24 polymul over 8 (2^21 per rank)
-    # 6.8 -> 8.0 ms with 4 pieces (half-empty launches).  Column pieces only have to cover the last
-    # row piece's exchange, so they may be smaller: 2^24 over 2 virtual ranks with 4 x 4 pieces (2^21
-    # elements per column piece) cost 1.5 % over 1 x 1, 2^24 over 8 with 2 x 2 (2^20) 11 %
-    # (profiles/r03_pieces/).
+    # Default: ONE whole-block exchange per transform (1 x 1 pieces).  On one GPU the pieces never
+    # measured a clear gain: 2^24 over 2 virtual ranks 2.18 / 2.16 / 2.21 ms for 1x1 / 2x1 / 4x4, and
+    # C4 over 8 with 4 x 4 pieces ran 33.4 ms in one refresh and 43.4 / 45.0 ms in the next two while
+    # C5 with 4 x 4 was slower than 1 x 1 (9.75 vs 8.82 ms; profiles/r03_final/configs.jsonl).  The
+    # virtual-rank exchange is device copies competing with the transforms for the same HBM, so what
+    # pieces hide over xGMI is only measurable on a multi-GPU node; until then they are opt-in
+    # (``pieces`` / ``col_pieces``, bench.py --pieces / --col-pieces).  When enabled, a piece's row
+    # transforms must still fill the GPU (one 1024-element tile per workgroup; 256 CUs x 4 resident
+    # workgroups), hence the minimum piece sizes below.
     MIN_PIECE_ELEMS = 1 << 22
     MIN_COL_PIECE_ELEMS = 1 << 21
 
     @classmethod
     def auto_pieces(cls, local_n: int, cap: int = 8, min_elems: Optional[int] = None) -> int:
+        """Largest power-of-two piece count (<= cap) keeping >= min_elems elements per piece; used only
+        when pieces are requested as "auto" (DistNTT(pieces="auto"))."""
         m = cls.MIN_PIECE_ELEMS if min_elems is None else min_elems
         k = 1
         while k < cap and local_n // (2 * k) >= m:
@@ -349,8 +352,9 @@ class DistNTT:
                  col_pieces: Optional[int] = None):
         """host_exchange: stage the all-to-all through host memory over a gloo group (rehearsing
         several ranks on ONE GPU, where RCCL refuses duplicate devices); never the product path.
-        pieces / col_pieces: row / column pieces of the pipelined exchange (None: auto_pieces of the
-        local share: >= 2^22 elements per row piece, >= 2^21 per column piece, at most 4 of those)."""
+        pieces / col_pieces: row / column pieces of the pipelined exchange (None: 1, one whole-block
+        exchange; "auto": auto_pieces of the local share, >= 2^22 elements per row piece, >= 2^21 per
+        column piece, at most 4 of those)."""
         import torch.distributed as dist
         self.dist = dist
         self.group = group
@@ -366,8 +370,9 @@ class DistNTT:
         ln = self.layout.local_n  # world 1: no exchange to hide
         auto_r = 1 if world == 1 else self.auto_pieces(ln)
         auto_c = 1 if world == 1 else self.auto_pieces(ln, cap=4, min_elems=self.MIN_COL_PIECE_ELEMS)
-        self.fs = FourStep(self.layout, self.engine, self, pieces=auto_r if pieces is None else pieces,
-                           col_pieces=auto_c if col_pieces is None else col_pieces)
+        pieces = 1 if pieces is None else (auto_r if pieces == "auto" else int(pieces))
+        col_pieces = 1 if col_pieces is None else (auto_c if col_pieces == "auto" else int(col_pieces))
+        self.fs = FourStep(self.layout, self.engine, self, pieces=pieces, col_pieces=col_pieces)
         self.n = self.layout.n
         self.passes: List[int] = []  # per-transform schedules: see the row / column plans
         # exchange timing (set_profiling): one window per all-to-all, from the first piece's start to

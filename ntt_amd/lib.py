@@ -14,6 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NTT_LIB_PATH") or os.path.join(HERE, "libntt.so")
 
 NTT_OK = 0
+NTT_ERR_ARG, NTT_ERR_HIP, NTT_ERR_RCCL, NTT_ERR_FIELD, NTT_ERR_NODEV, NTT_ERR_DEVICE = -1, -2, -3, -4, -5, -6
 NTT_FIELD_P469762049 = 0
 NTT_FIELD_BN254_FR = 1
 NTT_FIELD_BLS12_381_FR = 2
@@ -66,6 +67,7 @@ PROTOTYPES = {
     "ntt_mplan_destroy": (C.c_int, [_vp]),
     "ntt_count_noncanonical": (C.c_int, [_vp, _vp, C.c_uint64, C.POINTER(C.c_uint64), _vp]),
     "ntt_plan_device_status": (C.c_int, [_vp, C.POINTER(C.c_uint)]),
+    "ntt_plan_set_watchdog": (C.c_int, [_vp, C.c_uint]),
     "ntt_shim_cache_clear": (None, []),
     "ntt_inverse_pointwise_batch": (C.c_int, [_vp, _vp, _vp, _vp, C.c_uint, _vp]),
     "ntt_twiddle_pack_ex": (C.c_int, [_vp, _vp, _vp, C.c_uint, C.c_uint, C.c_uint, C.c_uint64, C.c_int, C.c_uint64,

@@ -149,11 +149,17 @@ class NTTPlan:
 
     def device_status(self) -> int:
         """ntt_plan_device_status: bit 0 = a watchdog gave up (single launch / fused in-place digit
-        reversal); with the checked build (libntt_debug.so) 0x100 bounds, 0x200 non-canonical input,
-        0x400 lazy bound, 0x800 non-canonical output.  Blocking; clears the word."""
+        reversal; until this clears it, every call on the plan raises NTTError NTT_ERR_DEVICE); with
+        the checked build (libntt_debug.so) 0x100 bounds, 0x200 non-canonical input, 0x400 lazy bound,
+        0x800 non-canonical output.  Blocking (synchronises the device); clears the report."""
         v = C.c_uint()
         _L.check(self._lib.ntt_plan_device_status(self._h, C.byref(v)), "ntt_plan_device_status")
         return v.value
+
+    def set_watchdog(self, spins: int = 1 << 21) -> None:
+        """ntt_plan_set_watchdog: poll limit of the plan's inter-workgroup waits (0 = give up at once,
+        a test hook for the NTT_ERR_DEVICE path)."""
+        _L.check(self._lib.ntt_plan_set_watchdog(self._h, int(spins)), "ntt_plan_set_watchdog")
 
     def count_noncanonical(self, t: torch.Tensor, stream=None) -> int:
         """Number of elements of t that are not < p (the transforms' input contract); blocking."""

@@ -1,0 +1,51 @@
+"""bench.py's host logic on the CPU (no GPU calls): the launcher refuses more ranks than visible
+devices, the column-layout assembly of the post-timing parity check, and its closed-form KAT."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from ntt_amd.distributed import Layout  # noqa: E402
+
+
+def test_spawn_refuses_more_ranks_than_devices():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "NTT_BENCH_EXCHANGE")}
+    env["HIP_VISIBLE_DEVICES"] = ""  # no device visible, even on a GPU box
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2, (r.stdout, r.stderr)
+    assert "refusing" in r.stderr
+
+
+def test_assemble_columns_restores_natural_order():
+    for log_n, world, log_n2, tail in [(12, 2, 6, ()), (12, 4, 5, (4,)), (14, 8, 7, (6,))]:
+        n = 1 << log_n
+        X = torch.arange(n * (int(np.prod(tail)) if tail else 1), dtype=torch.int64).reshape((n,) + tail)
+        parts = []
+        for g in range(world):
+            L = Layout(log_n, world, g, log_n2)
+            idx = torch.tensor([L.col_global(i) for i in range(L.local_n)])
+            parts.append(X[idx])
+        L = Layout(log_n, world, 0, log_n2)
+        assert torch.equal(bench.assemble_columns(parts, L.n1, L.c), X)
+
+
+def test_kat_check_matches_the_definition():
+    from ntt_amd.fields import field_params
+    for fid, log_n in [(0, 6), (1, 5), (2, 4)]:
+        p, g = field_params(fid)
+        n = 1 << log_n
+        w = pow(g, (p - 1) // n, p)
+        X = [sum(j * pow(w, j * k, p) for j in range(n)) % p for k in range(n)]
+        ks = list(range(n))
+        assert bench._kat_check(fid, log_n, 4, X, ks)
+        bad = list(X)
+        bad[3] = (bad[3] + 1) % p
+        assert not bench._kat_check(fid, log_n, 4, bad, ks)
+        assert bench._to_ints(torch.tensor([[5, 0, 0, 0], [-1, 1, 0, 0]])) == [5, (1 << 64) - 1 + (1 << 64)]

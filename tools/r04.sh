@@ -1,0 +1,39 @@
+#!/bin/bash
+# Round-4 GPU session steps (run from the repo root on the box via gpurun).  Every GPU step has its own
+# time limit; the first failure ends the session.  Usage: TAG=r04_x tools/r04.sh step [step ...]
+set -o pipefail
+export TMPDIR=/tmp
+TAG=${TAG:-r04}
+O=gpurun_out/$TAG
+mkdir -p $O
+step() {  # name seconds cmd...
+  local name=$1 t=$2; shift 2
+  echo "[r04] $name" >&2
+  timeout -k 10 "$t" "$@" > $O/$name.log 2>&1
+  local rc=$?
+  echo "[r04] $name rc=$rc" >&2
+  if [ $rc -ne 0 ]; then tail -40 $O/$name.log >&2; exit $rc; fi
+}
+PYT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
+for s in "$@"; do
+  case $s in
+    new) step pytest_new 400 $PYT tests/test_gpu_mplan_copy.py tests/test_gpu_watchdog.py ;;
+    dist) step pytest_dist 600 $PYT tests/test_gpu_distributed.py tests/test_gpu_polymul_dist.py tests/test_gpu_mplan_faults.py tests/test_gpu_mplan_copy.py ;;
+    tests) step pytest_gpu 1100 $PYT tests -m gpu ;;
+    smoke) step smoke 120 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    reh2) step bench_n2_rehearsal 400 env NTT_BENCH_EXCHANGE=host python3 -u bench.py --gpus 2 --steps 20 --warmup 10 ;;
+    reh8) step bench_n8_rehearsal 600 env NTT_BENCH_EXCHANGE=host python3 -u bench.py --gpus 8 --steps 10 --warmup 5 ;;
+    bench) step bench 300 python3 -u bench.py ;;
+    benchd) step bench_driver 300 python3 -u bench.py --steps 20 --warmup 5 ;;
+    fs1) step bench_fourstep_w1 300 python3 -u bench.py --four-step --steps 20 --warmup 10 --no-cpu-baseline ;;
+    prof) step rocprof_stats 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py ;;
+    pmc)
+      step pmc_sq 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d $O/pmc/sq -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity
+      step pmc_fetch 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/pmc/fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity
+      step pmc_write 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc/write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity
+      step traffic 60 python -u tools/pmc_to_traffic.py $O/pmc f1_L4_n24_w1 $O/pmc_summary.json ;;
+    configs) step configs 600 python -u tools/bench_configs.py --out $O/configs.jsonl ;;
+    *) echo "unknown step $s" >&2; exit 2 ;;
+  esac
+done
+echo "[r04] done" >&2
