@@ -96,6 +96,9 @@ def parse():
                     help="four-step: column pieces whose transforms start as their part of the all-to-all "
                          "arrives (default 1; 'auto')")
     ap.add_argument("--no-parity", action="store_true", help="skip the post-timing parity check")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="N > 1: skip the secondary timings after the headline (pipelined pieces, independent "
+                         "transforms per rank)")
     ap.add_argument("--independent", action="store_true",
                     help="N > 1: one independent transform per rank (weak scaling, no data-path collective)")
     ap.add_argument("--cpu-log-n", type=int, default=22, help="C-oracle single-core sample size (log2)")
@@ -316,6 +319,61 @@ def parity_single(args, plan):
             "checked": f"x_j = j against the closed-form KAT at {len(ks)} sampled k; inverse(forward(B)) == B"}
 
 
+def _timed(step, steps: int, warmup: int, barrier, dist, dev: str) -> float:
+    """ms per step over `steps` calls after `warmup`, barrier + synchronize on both sides, max over ranks."""
+    import torch
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - t0
+    tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return float(tt.item()) / steps * 1e3
+
+
+def secondary_timings(args, eng, dist, rccl, local, barrier):
+    """After the headline: (a) the same distributed transform with the pipelined exchange pieces of
+    DistNTT.auto_pieces, (b) one independent 2^log_n transform per rank.  Both timed like the
+    headline (fewer steps), each rank's time maxed over ranks."""
+    import torch
+    from ntt_amd.distributed import DistNTT
+    from ntt_amd.ntt import NTTPlan
+    dev = f"cuda:{local}" if rccl else "cpu"
+    steps, warm = max(5, min(args.steps, 30)), max(3, min(args.warmup, 20))
+    n = 1 << args.log_n
+    res = {}
+    L = eng.layout
+    ar = DistNTT.auto_pieces(L.local_n)
+    ac = DistNTT.auto_pieces(L.local_n, cap=4, min_elems=DistNTT.MIN_COL_PIECE_ELEMS)
+    if (ar, ac) != (len(eng.fs.pieces), eng.fs.cp):
+        e2 = DistNTT(field_id=args.field, log_n=args.log_n, limbs64=args.limbs, device=local,
+                     host_exchange=not rccl, pieces="auto", col_pieces="auto")
+        d2 = e2.empty()
+        e2.fill(d2, "random", seed=2)
+        ms = _timed(lambda: e2.forward(d2), steps, warm, barrier, dist, dev)
+        res["pipelined_pieces"] = {"row_pieces": len(e2.fs.pieces), "col_pieces": e2.fs.cp, "ms_per_step": ms,
+                                   "value": n / (ms * 1e-3), "steps": steps, "warmup": warm}
+        del e2, d2
+    else:
+        res["pipelined_pieces"] = {"skipped": f"auto pieces for {L.local_n} local elements are 1 x 1"}
+    pl = NTTPlan(field_id=args.field, log_n=args.log_n, limbs64=args.limbs, device=local)
+    x = pl.empty()
+    pl.fill(x, "random", seed=2 + L.rank)
+    ms = _timed(lambda: pl.forward(x), steps, warm, barrier, dist, dev)
+    res["independent"] = {"what": f"one 2^{args.log_n} transform per rank, {L.world} ranks at once (weak scaling)",
+                          "ms_per_step": ms, "value": L.world * n / (ms * 1e-3), "steps": steps, "warmup": warm}
+    del pl, x
+    torch.cuda.synchronize()
+    return res
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -496,6 +554,13 @@ def main():
             par = parity_single(args, plan) if rank == 0 else None
         if rank == 0:
             out["parity"] = par
+    # ---- secondary views for N > 1, outside the headline's timed region (same process group): the
+    # pipelined exchange pieces (opt-in until they measurably win) and one independent transform per
+    # rank (weak scaling, no data-path collective)
+    if four_step and world > 1 and not args.no_secondary:
+        sec = secondary_timings(args, eng, dist, rccl, local, barrier)
+        if rank == 0:
+            out["secondary"] = sec
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args.field, args.limbs if args.limbs != 1 else 1, args.cpu_log_n)

@@ -99,9 +99,10 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
  * bounded waits reported by ntt_plan_device_status); batched calls take a separate pass of disjoint
  * tile-pair swaps instead.  Same contract and results as the default schedule, within ~1 % of its
  * time on the 256-bit path.  P469762049 plans run on 8-B scratch elements for it (the default P
- * plan keeps 4-B ones).  The 6-limb 256-bit layout (48-B elements, 32-B scratch), sizes with no
- * palindrome the pass kernels accept (2^11 and 2^13 on the 1024-element tiles; P: 2^15, 2^17, 2^19
- * on its 8192-element tiles) and the rival schedules return NTT_ERR_ARG. */
+ * plan keeps 4-B ones); 6 x 64-bit plans of a modulus < 2^255 keep their intermediates in the
+ * caller's 48-B elements (the default 6-limb plan uses 32-B scratch).  Sizes with no palindrome the
+ * pass kernels accept (2^11 and 2^13 on the 1024-element tiles; P: 2^15, 2^17, 2^19 on its
+ * 8192-element tiles) and the rival schedules return NTT_ERR_ARG. */
 #define NTT_PLAN_IN_PLACE 16u
 /* Single-launch schedule (BASELINE config 2, "single-kernel self-sort-in-place"; the reference runs
  * 2^20 as 4 launches, GZKP-NTT.cu:1509-1545): a 3-pass forward / inverse of a 4-limb BN254 / BLS12-381
@@ -130,7 +131,10 @@ int ntt_plan_device_status(ntt_plan* plan, unsigned* bad);
 int ntt_plan_set_watchdog(ntt_plan* plan, unsigned spins);
 
 /* Modulus-generic plan, like big-num.cu's `prime` / `omega` kernel arguments (big-num.cu:68,173,260):
- * modulus and generator given as limbs64 little-endian 64-bit limbs. */
+ * modulus and generator given as limbs64 little-endian 64-bit limbs.  Accepted moduli: odd primes
+ * with 2^log_n | p - 1 and, by limb count, p < 2^30 (1 limb: lazy values up to 4p must fit 32 bits,
+ * so e.g. the 31-bit 2013265921 returns NTT_ERR_FIELD), p < 2^255 (4 limbs), p < 2^(29*14-6) with 2p
+ * below 2^383 (6 limbs). */
 int ntt_plan_create_custom(ntt_plan** out, const uint64_t* modulus, const uint64_t* generator, unsigned limbs64,
                            unsigned log_n, int device);
 

@@ -1,7 +1,7 @@
 // Field engines: how an element lives in registers, LDS, HBM and twiddle tables, and the lazy
 // butterfly arithmetic on it.  The NTT kernels are generic over the engine.
 //
-//   Eng29<L, W32>: radix-2^29 limbs (field29.hpp); HBM holds W32 canonical 32-bit words
+//   Eng29<L, W32[, SCR]>: radix-2^29 limbs (field29.hpp); HBM holds W32 canonical 32-bit words
 //                  (cgbn_mem_t<32*W32>, reference cgbn_cuda.h:51-55).  L = 9 / W32 = 8 is the 256-bit
 //                  class (BN254 Fr, BLS12-381 Fr, zero-padded P), L = 14 / W32 = 12 the 384-bit
 //                  (6 x 64-bit limb) template.
@@ -90,15 +90,17 @@ __device__ __forceinline__ void store_wt16(uint4* p, uint32_t a, uint32_t b, uin
 // Lazy bounds (units of p): the in-register DFTs take inputs < IN p (IN = 4: products < 3p,
 // reduced k = 0 outputs < 4p, HBM loads < p) and radix-2 stage s adds/subtracts with offset
 // IN 2^(s-1) p, so a Q-point DFT returns values < IN Q p <= 32p < B for every supported field.
-template <int L, int W32>
+template <int L, int W32, int SCR_ = 0>
 struct Eng29 {
   static constexpr int W = L;                   // registers per element
   static constexpr int MEMW = W32;              // 32-bit words per element in HBM (canonical)
-  // words per element of the plan's own scratch and outer-twiddle tables: 256-bit values (< 2p, p <
-  // 2^255) need 8 even in the 48-B caller layout, so only the first read and the last write of a
-  // transform move 48 B per element
-  static constexpr int SCRW = (L <= 9 && W32 > 8) ? 8 : W32;
-  static constexpr int TABW = SCRW;  // words per entry of the element-format twiddle tables
+  // words per element of the plan's own scratch: 256-bit values (< 2p, p < 2^255) need 8 even in the
+  // 48-B caller layout, so only the first read and the last write of a transform move 48 B per
+  // element.  SCR_ != 0 forces it (Eng256wI: the caller's 48-B element, for NTT_PLAN_IN_PLACE plans,
+  // whose intermediates live in the caller's buffer)
+  static constexpr int SCRW = SCR_ ? SCR_ : ((L <= 9 && W32 > 8) ? 8 : W32);
+  // words per entry of the element-format twiddle tables (values < p: 8 words for the 256-bit class)
+  static constexpr int TABW = (L <= 9) ? 8 : W32;
   static constexpr int TW = (2 * L + 3) & ~3;   // words per twiddle-table entry: w, ws (16-B aligned)
   static constexpr int LDSW = L;                // words per element in LDS
   static constexpr int IN = 4;                  // DFT input bound (units of p)

@@ -1,0 +1,5 @@
+// Eng256wI (NTT_PLAN_IN_PLACE plans of the 48-B layout): k_pass instantiations for KIND_COLUMN.
+#include "ntt_kernels_impl.hpp"
+namespace ntt {
+NTT_INSTANTIATE_KIND(Eng256wI, KIND_COLUMN)
+}  // namespace ntt

@@ -252,11 +252,12 @@ static bool schedule_palindrome(unsigned log_n, unsigned tile_log, unsigned rmax
 template <class E>
 struct EngHost;
 
-template <int L, int W32>
-struct EngHost<Eng29<L, W32>> {
+template <int L, int W32, int S>
+struct EngHost<Eng29<L, W32, S>> {
+  using E29 = Eng29<L, W32, S>;
   static constexpr int NH = W32;
-  static constexpr int TW = Eng29<L, W32>::TW;
-  using EA = typename Eng29<L, W32>::Args;
+  static constexpr int TW = E29::TW;
+  using EA = typename E29::Args;
   HostField<NH> const* H = nullptr;
   Vec<NH> kR{};          // B = 2^(29L) mod p, canonical
   uint32_t pinvB[L] = {};  // p^-1 mod B
@@ -309,7 +310,7 @@ struct EngHost<Eng29<L, W32>> {
     for (int i = 0; i < 5; ++i) inv *= 2 - p[0] * inv;
     A.M.pinv = (0u - inv) & kMask29;
     uint32_t tmp[TW];
-    auto to_tw = [&](const Vec<NH>& c, typename Eng29<L, W32>::Tw& t) {
+    auto to_tw = [&](const Vec<NH>& c, typename E29::Tw& t) {
       encode(c, tmp);
       for (int i = 0; i < L; ++i) {
         t.w[i] = tmp[i];
@@ -336,7 +337,6 @@ struct EngHost<Eng29<L, W32>> {
       for (int i = 1; i + 1 < L; ++i) c[i] = kp[i] + pad - b;
       c[L - 1] = kp[L - 1] - b;
     };
-    using E29 = Eng29<L, W32>;
     padded(5, 1u << 29, A.pc[E29::PC_5_29]);
     padded(9, 1u << 30, A.pc[E29::PC_9_30]);
     padded(4, 1u << 29, A.pc[E29::PC_4_29]);
@@ -747,16 +747,25 @@ struct PlanImpl final : PlanBase {
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return NTT_OK;
     if (2 * elems * TABW * 4 > free_b / 4) return NTT_OK;  // both directions within a quarter of free HBM
-    if (int rc = ensure_full(0)) return rc;
+    if (int rc = ensure_full(0, nullptr)) return rc;
+    if (hipDeviceSynchronize() != hipSuccess) return NTT_ERR_HIP;  // plan creation is synchronous
     use_full = true;
     return build_shoup_tables();
   }
-  // the per-pass tables of one direction (the inverse's pass-1 table carries n^-1)
-  int ensure_full(int dir) {
-    if (d_fulls[dir]) return NTT_OK;
+  // The per-pass tables of one direction (the inverse's pass-1 table carries n^-1), built on `st`.
+  // The forward's are built at plan creation, the inverse's at the first inverse call (a forward-only
+  // plan never holds them): that build is enqueued on the call's stream ahead of its passes, with no
+  // device-wide synchronisation.  If the allocation fails then, the direction keeps its two-level
+  // tables (one more product per element in pass 1) instead of failing the call.
+  bool full_failed[2] = {false, false};
+  int ensure_full(int dir, hipStream_t st) {
+    if (d_fulls[dir] || full_failed[dir]) return NTT_OK;
     if (hipMalloc(&d_fulls[dir], full_elems * TABW * 4) != hipSuccess) {
       d_fulls[dir] = nullptr;
-      return NTT_ERR_HIP;
+      (void)hipGetLastError();  // clear the sticky allocation error
+      if (dir == 0) return NTT_ERR_HIP;  // at creation: the plan reports it
+      full_failed[dir] = true;
+      return NTT_OK;
     }
     unsigned blk = log_n;
     for (unsigned i = 0; i + 1 < npass; ++i) {
@@ -764,11 +773,11 @@ struct PlanImpl final : PlanBase {
       const uint32_t* hi = d_tab + (dir ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
       // column-group-major layout of the pass kernel's tiles (T = TILE / R columns per workgroup)
       if (launch_build_tw<E>(d_fulls[dir] + full_off[i] * TABW, 1ull << blk, r[i], tile_log_of<E>() - r[i], log_n - blk,
-                             lo, hi, lo_bits, dir ? Fi : Ff, nullptr) != hipSuccess)
+                             lo, hi, lo_bits, dir ? Fi : Ff, st) != hipSuccess)
         return NTT_ERR_HIP;
       blk -= r[i];
     }
-    return hipDeviceSynchronize() == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+    return NTT_OK;
   }
 
   // Column passes 2..p-1 whose table is small enough to stay in L2 (N_i entries of E::TW words <=
@@ -1042,7 +1051,8 @@ struct PlanImpl final : PlanBase {
       }
       const uint32_t grid = (uint32_t)((n << il) >> tile_log_of<E>());
       if (use_full)
-        if (int rc = ensure_full(inverse ? 1 : 0)) return rc;
+        if (int rc = ensure_full(inverse ? 1 : 0, st)) return rc;
+      const bool full_dir = use_full && d_fulls[inverse ? 1 : 0];  // else: the two-level tables
       // the passes' arguments: column passes 0..npass-2, then the final pass
       PassArgs<E> PA[8];
       unsigned blk = log_n;
@@ -1058,7 +1068,7 @@ struct PlanImpl final : PlanBase {
           const char* v = getenv("NTT_PASS1_FULL");
           return v && atoi(v) > 0;
         }();
-        A.tw_full = (use_full && (i > 0 || E::PASS1_FULL_TABLE || p1_full)) ? d_fulls[inverse ? 1 : 0] + full_off[i] * TABW
+        A.tw_full = (full_dir && (i > 0 || E::PASS1_FULL_TABLE || p1_full)) ? d_fulls[inverse ? 1 : 0] + full_off[i] * TABW
                                                                              : nullptr;
         if (i > 0 && d_full_sh && full_sh_ok[i]) {
           A.tw_full = d_full_sh + full_sh_off[inverse ? 1 : 0][i] * TW;
@@ -1306,7 +1316,7 @@ struct PlanImpl final : PlanBase {
     if (!inverse) return NTT_ERR_ARG;  // the product is taken at the inverse's load
     const size_t count = (size_t)n * ((io.fs & FS_IL) ? (1ull << io.il) : batch);
     if (polymul_fusable() && npass >= 2) {  // in2 read through the input map like in
-      if (int rc = ensure_polymul_table()) return rc;
+      if (int rc = ensure_polymul_table(st)) return rc;
       return run_io(pin, static_cast<const uint32_t*>(in2), pout, batch, true, st, nullptr, nullptr, &io);
     }
     if (!(io.fs & (FS_MAP_IN | FS_MAP_OUT))) {  // same layout in and out: the product in place in out
@@ -1355,7 +1365,8 @@ struct PlanImpl final : PlanBase {
     }
   }
   // Inverse pass-1 outer-twiddle table scaled by n^-1 R_e (built on first use, same layout as d_full).
-  int ensure_polymul_table() {
+  // Built on the call's stream ahead of the passes that read it (no device-wide synchronisation).
+  int ensure_polymul_table(hipStream_t st) {
     if (d_full_pm) return NTT_OK;
     const size_t elems = 1ull << log_n;
     if (hipMalloc(&d_full_pm, elems * TABW * 4) != hipSuccess) {
@@ -1363,8 +1374,7 @@ struct PlanImpl final : PlanBase {
       return NTT_ERR_HIP;
     }
     if (launch_build_tw<E>(d_full_pm, elems, r[0], tile_log_of<E>() - r[0], 0, d_tab + off_los_i,
-                           d_tab + off_hi_ipm, lo_bits, Fi, nullptr) != hipSuccess ||
-        hipDeviceSynchronize() != hipSuccess)
+                           d_tab + off_hi_ipm, lo_bits, Fi, st) != hipSuccess)
       return NTT_ERR_HIP;
     return NTT_OK;
   }
@@ -1389,7 +1399,7 @@ struct PlanImpl final : PlanBase {
     auto pa = static_cast<const uint32_t*>(a), pb = static_cast<const uint32_t*>(b);
     auto pc = static_cast<uint32_t*>(c);
     if (polymul_fusable()) {
-      if (int rc = ensure_polymul_table()) return rc;
+      if (int rc = ensure_polymul_table(st)) return rc;
       return run_io(pa, pb, pc, batch, true, st);
     }
     if (int rc = pointwise_n(pa, pb, pc, (size_t)n * batch, st)) return rc;
@@ -1484,7 +1494,12 @@ static int make_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, const 
   } else if (limbs64 == 6) {
     // the 384-bit element layout: 256-bit arithmetic when the modulus allows it (BN254 Fr,
     // BLS12-381 Fr: the upper two 64-bit limbs of every element are zero), 14 limbs otherwise
-    if (p64[4] == 0 && p64[5] == 0 && (p64[3] >> 63) == 0) {
+    if (p64[4] == 0 && p64[5] == 0 && (p64[3] >> 63) == 0 && (flags & NTT_PLAN_IN_PLACE)) {
+      // in place: the intermediates live in the caller's 48-B elements (no 32-B plan scratch)
+      auto impl = std::make_unique<PlanImpl<Eng256wI>>();
+      rc = impl->init(p32, g32, log_n, device, flags);
+      out = std::move(impl);
+    } else if (p64[4] == 0 && p64[5] == 0 && (p64[3] >> 63) == 0) {
       auto impl = std::make_unique<PlanImpl<Eng256w>>();
       rc = impl->init(p32, g32, log_n, device, flags);
       out = std::move(impl);

@@ -162,6 +162,41 @@ def test_in_place_384bit_class():
         assert np.array_equal(_host(t, 6), x), log_n
 
 
+@pytest.mark.parametrize("fid,log_n", [(2, 12), (1, 16), (2, 20), (1, 23)])
+def test_in_place_6limb_layout_matches_oracle_and_default(fid, log_n):
+    """C3's 6 x 64-bit layout in place (VERDICT r03 item 7): the intermediates live in the caller's
+    48-B elements (Eng256wI), 256-bit arithmetic; equal to the default 6-limb plan and to the oracle."""
+    p, g = R.FIELDS[fid]
+    ip = _plan(fid, log_n, 6)
+    df = _plan(fid, log_n, 6, in_place=False)
+    assert _is_palindrome(ip.passes) and sum(ip.passes) == log_n, ip.passes
+    a = ip.fill(ip.empty(), "random", seed=600 + log_n)
+    b = a.clone()
+    x = _host(a, 6).copy()
+    ip.forward(a)
+    df.forward(b)
+    assert torch.equal(a, b), (fid, log_n, ip.passes, df.passes)
+    if log_n <= 20:
+        assert np.array_equal(_host(a, 6), OC.ntt_mp_par(x, p, g, THREADS))
+    ip.inverse(a)
+    assert np.array_equal(_host(a, 6), x)
+
+
+def test_in_place_6limb_2pow24_bls_elementwise():
+    """BASELINE C3 (2^24 BLS12-381 Fr, 6 x 64-bit limbs) in place: forward and inverse element by
+    element against the threaded C oracle (GZKP-NTT.cu:30-48 restated; inverse GZKP-NTT.cu:1725-1732)."""
+    p, g = R.FIELDS[2]
+    ip = _plan(2, 24, 6)
+    assert ip.passes == [8, 8, 8]
+    a = ip.fill(ip.empty(), "random", seed=3)
+    x = _host(a, 6).copy()
+    ip.forward(a)
+    assert np.array_equal(_host(a, 6), OC.ntt_mp_par(x, p, g, THREADS))
+    a.copy_(torch.from_numpy(x.view(np.int64)).to(a.device))
+    ip.inverse(a)
+    assert np.array_equal(_host(a, 6), OC.ntt_mp_par(x, p, g, THREADS, inverse=True))
+
+
 GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "ref_p469762049.npz"))
 
 
@@ -195,7 +230,6 @@ def test_in_place_p_path_vs_reference_outputs(log_n):
 
 
 @pytest.mark.parametrize("kw", [dict(fid=0, log_n=15, L=1),            # P: no palindrome with r_1 + r_p >= 13
-                                dict(fid=1, log_n=16, L=6),            # 6-limb 256-bit: 32-B scratch, 48-B elements
                                 dict(fid=1, log_n=11, L=4),            # no palindrome with r_1 + r_p >= 10
                                 dict(fid=1, log_n=13, L=4),            # ... and r_{p-1} + r_p >= 10
                                 dict(fid=1, log_n=16, L=4, stockham=True)])

@@ -246,6 +246,23 @@ def test_custom_modulus_matches_builtin():
     assert torch.equal(ta, tb)
 
 
+def test_one_limb_modulus_range():
+    """1-limb plans take odd primes p < 2^30 (include/ntt.h: the lazy values up to 4p fit 32 bits).
+    A 31-bit NTT prime (2013265921 = 15 2^27 + 1) is refused with NTT_ERR_FIELD; the largest 30-bit
+    one in range works and matches the oracle."""
+    from ntt_amd import lib as Lb
+    from ntt_amd.ntt import NTTPlan
+    with pytest.raises(Lb.NTTError) as ei:
+        NTTPlan(log_n=10, limbs64=1, modulus=2013265921, generator=31)
+    assert ei.value.status == Lb.NTT_ERR_FIELD
+    p, g = 1004535809, 3  # 479 2^21 + 1 < 2^30
+    pl = NTTPlan(log_n=12, limbs64=1, modulus=p, generator=g)
+    x = OC.random_limbs(0, 1 << 12, seed=30, L=1)[:, 0].astype(np.int64) % p
+    t = torch.from_numpy(x).to("cuda:0")
+    pl.forward(t)
+    assert np.array_equal(t.cpu().numpy(), OC.ntt_u64(x, p, g))
+
+
 @pytest.mark.parametrize("fid,L,log_n,batch", [(1, 4, 12, 3), (2, 6, 12, 3), (1, 6, 17, 2), (0, 1, 15, 3)])
 def test_batch_forward(fid, L, log_n, batch):
     """Batched transforms (the 48-B layout with 17 = 6+6+5 also runs a scratch-to-scratch pass)."""

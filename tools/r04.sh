@@ -32,6 +32,10 @@ for s in "$@"; do
       step pmc_fetch 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/pmc/fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity
       step pmc_write 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc/write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity
       step traffic 60 python -u tools/pmc_to_traffic.py $O/pmc f1_L4_n24_w1 $O/pmc_summary.json ;;
+    limb30)
+      step limb30_prep 60 python tools/mb_limb30_check.py prep $O/limb30
+      step limb30_run 300 tools/mb_limb30 $O/limb30/consts.bin $O/limb30/xs.bin $O/limb30/rs.bin
+      step limb30_verify 120 python tools/mb_limb30_check.py verify $O/limb30 ;;
     configs) step configs 600 python -u tools/bench_configs.py --out $O/configs.jsonl ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
   esac
