@@ -95,6 +95,8 @@ def parse():
     ap.add_argument("--col-pieces", default=None,
                     help="four-step: column pieces whose transforms start as their part of the all-to-all "
                          "arrives (default 1; 'auto')")
+    ap.add_argument("--prewarm-s", type=float, default=0.3,
+                    help="after --warmup, keep stepping (untimed) until the warmup lasted this long (clock ramp)")
     ap.add_argument("--no-parity", action="store_true", help="skip the post-timing parity check")
     ap.add_argument("--no-secondary", action="store_true",
                     help="N > 1: skip the secondary timings after the headline (pipelined pieces, independent "
@@ -435,6 +437,24 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    # Clock ramp: the GPU's clocks settle over the first ~25 transforms, or ~0.3 s, after
+    # start-up or idle; a short --warmup (the driver's 5) would time the ramp, not the steady state.
+    # Keep stepping, untimed, until the warmup has lasted PREWARM_S of GPU time (reported as
+    # warmup_run); the timed region below is still exactly --steps steps.
+    # N > 1: the ranks decide together, chunk by chunk, so every rank runs the same steps (they exchange).
+    extra, t_w = 0, time.perf_counter()
+    while args.prewarm_s > 0 and extra < 4000:
+        go = time.perf_counter() - t_w < args.prewarm_s
+        if use_dist:
+            g = torch.tensor([1 if go else 0], dtype=torch.int64, device=f"cuda:{local}" if rccl else "cpu")
+            dist.all_reduce(g, op=dist.ReduceOp.MAX)
+            go = bool(g.item())
+        if not go:
+            break
+        for _ in range(8):
+            step()
+        extra += 8
+        torch.cuda.synchronize()
 
     # ---- timed region: K steps bracketed by barrier + synchronize; per-launch HIP events recorded
     # on the launch stream between kernels (ntt_plan_set_profiling) accumulate per-launch times.
@@ -472,6 +492,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "warmup_run": args.warmup + extra,  # untimed steps actually run (the clock-ramp pre-warm included)
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
         "scaling": "strong" if four_step else "weak",

@@ -62,14 +62,18 @@ struct FsMap {
   }
 };
 
-// Every inter-workgroup wait (k_final_ipn, k_fused3, k_fused3b) is bounded.  A wait that reaches
-// `spins` polls gives up: it raises the launch's own abort word (so the launch's other waits give up
-// at once and every wave reaches the exit), the workgroup skips its remaining stores, and the plan's
+// Every inter-workgroup wait (k_final_ipn, k_fused3, k_fused3b, k_fused3bi) is bounded.  A wait that
+// reaches `spins` polls gives up: it raises the launch's own abort word (which the launch's other
+// waits check every 256 polls, so they give up too and every wave reaches the exit), the workgroup
+// skips its remaining stores, and the plan's
 // host-mapped report word `report` is set (system scope).  The next call on the plan returns
 // NTT_ERR_DEVICE without any device query (ntt_plan_device_status reads and clears the report).
 // spins = 0 gives up at once (ntt_plan_set_watchdog: a test hook).
 struct Watchdog {
   uint32_t* report;  // host-mapped word of the plan (null: none)
+  uint32_t* abort;   // the launch's abort word, on a 128-B line of its own (pollers of a line that also
+                     // holds a counter queue the counter's atomic adds: DESIGN §4); zeroed by the last
+                     // workgroup out
   uint32_t spins;    // poll limit, ~1 us per poll after the first few (default 2^21, ~2 s)
 };
 
@@ -114,12 +118,13 @@ struct PassArgs {
   uint32_t tw_sh;          // column pass: tw_full holds Shoup pairs (canonical w, floor(w B / p); E::TW words
                            // per entry, E::SHOUP_OUTER engines) instead of w R_e in the element format
   // ---- in-place final pass with the digit reversal fused (k_final_ipn, NTT_PLAN_IN_PLACE):
-  uint32_t* ipn_sync;        // [0] tile ticket, [1] workgroups exited, [2] this launch gave up a wait;
-                             // slab m: reads done at [32 (1 + m)], ready at [32 (1 + m) + 1] (one 128-B
-                             // line per slab)
+  uint32_t* ipn_sync;        // [0] tile ticket, [1] workgroups exited; slab m: reads done at [32 (1 + m)],
+                             // ready at [32 (1 + m) + 1] (one 128-B line per slab)
   const uint32_t* ipn_order; // slab (middle-digit value) of the i-th slab in ticket order (pairs adjacent)
   uint32_t ipn_strips;       // workgroups per slab (R_1 / T)
-  Watchdog wd;               // bounded waits (k_final_ipn)
+  uint32_t* ipn_go;          // k_fused3bi (the in-place single launch): the final pass's barrier go word
+                             // (ipn_sync: the launch's sync words, ipn_strips: that barrier's arrival target)
+  Watchdog wd;               // bounded waits (k_final_ipn, k_fused3bi)
   // debug builds (NTT_DEBUG_CHECKS): element extents of src / dst from this transform's first element
   // (~0: not checked, e.g. four-step maps into the caller's exchange blocks)
   size_t dbg_src_n, dbg_dst_n;
@@ -130,7 +135,7 @@ enum : uint32_t { FS_MAP_IN = 1u, FS_MAP_OUT = 2u, FS_IL = 4u, FS_MAP_EPI = 8u }
 // one persistent launch runs pass 1's, pass 2's and the final pass's tiles, handed between
 // workgroups through counters instead of kernel boundaries.  Word layout of `sync` (zero before the
 // first launch; the last workgroup to leave re-zeroes it): [0] tile ticket, [1] workgroups exited,
-// [2] abort (non-zero: a dependency wait of this launch gave up), [3] spare, [4, 4 + n12) pass 1 -> 2 counters,
+// [2], [3] spare, [4, 4 + n12) pass 1 -> 2 counters,
 // [4 + n12, 4 + n12 + n23) pass 2 -> final counters, then one ready word per counter (rbase).
 struct FusedArgs {
   uint32_t* sync;
@@ -147,7 +152,8 @@ struct FusedArgs {
   uint32_t dbg;                // diagnostics only (NTT_FUSED_DBG): bit 0 no dependency waits (wrong
                                // output), bit 2 static tile order (needs every workgroup resident)
   uint32_t mode;               // 0: dataflow hand-offs between tiles (k_fused3); 1: two grid barriers
-                               // over a cooperative launch (k_fused3b)
+                               // over a cooperative launch (k_fused3b); 2: the NTT_PLAN_IN_PLACE form,
+                               // three grid barriers, one workgroup per tile (k_fused3bi)
   Watchdog wd;                 // bounded waits; sync[2] is the launch's abort word
 };
 template <class E>

@@ -327,26 +327,26 @@ __device__ __forceinline__ void ipn_signal_read(const PassArgs<E>& A, uint32_t m
 }
 // A wait gave up (Watchdog, ntt_kernels.hpp): the launch's abort word, then the plan's host-mapped
 // report word (system scope: the host reads it at the plan's next call without a device query).
-__device__ __forceinline__ void watchdog_trip(uint32_t* abort_w, const Watchdog& wd) {
-  __hip_atomic_store(abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void watchdog_trip(const Watchdog& wd) {
+  if (wd.abort) __hip_atomic_store(wd.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (wd.report) __hip_atomic_store(wd.report, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 // One lane's bounded poll of `word` with relaxed agent-scope global loads (no read-modify-write
 // polls: DESIGN §4), sleeping S0 below N0 polls, S1 below N1, S2 after.  True once the word is
 // non-zero; false when the wait gave up: wd.spins polls without it (this lane trips the watchdog) or
-// another workgroup of the launch gave up first (its abort word is set).
+// another workgroup of the launch gave up first (its abort word, checked every 256 polls, is set).
 template <int S0, uint32_t N0, int S1, uint32_t N1, int S2>
-__device__ __forceinline__ bool poll_bounded(uint32_t* word, uint32_t* abort_w, const Watchdog& wd) {
+__device__ __forceinline__ bool poll_bounded(uint32_t* word, const Watchdog& wd) {
   typedef __attribute__((address_space(1))) uint32_t gu32;  // a global (not flat) access
   gu32* const g = (gu32*)word;
-  gu32* const ab = (gu32*)abort_w;
+  gu32* const ab = (gu32*)wd.abort;
   for (uint32_t spins = 0;; ++spins) {
     if (__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return true;
     if (spins >= wd.spins) {
-      watchdog_trip(abort_w, wd);
+      watchdog_trip(wd);
       return false;
     }
-    if (spins >= 16 && __hip_atomic_load(ab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+    if ((spins & 255u) == 255u && ab && __hip_atomic_load(ab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
     if (spins < N0) __builtin_amdgcn_s_sleep(S0);
     else if (spins < N1) __builtin_amdgcn_s_sleep(S1);
     else __builtin_amdgcn_s_sleep(S2);
@@ -358,9 +358,36 @@ template <class E>
 __device__ __forceinline__ bool ipn_wait_mirror(const PassArgs<E>& A, uint32_t midrev) {
   __shared__ uint32_t s_ok;
   if (threadIdx.x == 0)
-    s_ok = poll_bounded<4, 8, 32, 8, 32>(A.ipn_sync + 32 * (1 + midrev) + 1, A.ipn_sync + 2, A.wd) ? 1u : 0u;
+    s_ok = poll_bounded<4, 8, 32, 8, 32>(A.ipn_sync + 32 * (1 + midrev) + 1, A.wd) ? 1u : 0u;
   __syncthreads();
-  return s_ok != 0u;
+  return __builtin_amdgcn_readfirstlane(s_ok) != 0u;  // wave-uniform: scalar branches around it
+}
+
+// Grid-wide barrier over a cumulative arrival counter (barrier k of a launch completes at k G
+// arrivals), the guide's R1 publish (MI355X_MICROARCH.md § visibility): every wave drains its
+// (write-through) stores, a workgroup barrier, one lane's agent-scope add; the last arrival raises the
+// barrier's go word (a 128-B line of its own); one lane polls it (bounded, Watchdog), ONE agent-scope
+// acquire, and the workgroup barrier releases every wave.  False (workgroup-uniform) when the wait
+// gave up: the workgroup then skips what is left of the launch.
+__device__ __forceinline__ bool grid_barrier_words(uint32_t* counter, uint32_t* go, uint32_t target, const Watchdog& wd) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores (and loads) are done
+  __syncthreads();
+  __shared__ uint32_t s_ok;
+  if (threadIdx.x == 0) {
+    if (__hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == target - 1)
+      __hip_atomic_store(go, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_ok = poll_bounded<4, 16, 32, 16, 32>(go, wd) ? 1u : 0u;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  return __builtin_amdgcn_readfirstlane(s_ok) != 0u;
+}
+// The in-place single launch's third barrier, between every final tile's loads and any store
+// (PassArgs: ipn_sync = the launch's sync words, ipn_go = the go word, ipn_strips = the arrival target)
+template <class E>
+__device__ __forceinline__ bool ipn_grid_barrier(const PassArgs<E>& A) {
+  return grid_barrier_words(A.ipn_sync, A.ipn_go, A.ipn_strips, A.wd);
 }
 
 // LDS of one pass tile (words), and whether the pass stages its w_R^e table in LDS: E::LDS_TW
@@ -386,11 +413,12 @@ __host__ __device__ constexpr bool pass_ltw() {
 // LOOPED (persistent workgroups, k_fused3): the thread index is re-read per tile through an opaque
 // copy, so that the compiler does not hoist every lane-dependent address out of the tile loop (held in
 // VGPRs across the whole loop, they spilled 200-380 B per thread; per tile they cost a few VALU ops).
-// IPN (final pass of an in-place plan, k_final_ipn): outputs go to their natural positions in the same
-// buffer; a tile's loads are counted in per slab, and its stores wait until the mirror slab has been
-// read (see k_final_ipn).
+// IPN (final pass of an in-place plan): outputs go to their natural positions in the same buffer.
+// 1 (k_final_ipn): a tile's loads are counted in per slab, and its stores wait until the mirror slab
+// has been read.  2 (k_fused3bi, every final tile resident): a grid barrier between all loads and all
+// stores.
 template <class E, int LOGR, int KIND, bool FULLTW, bool FAST, int PRO = PRO_NONE, bool SRC_USER = true,
-          int FSM = 0, bool SHTW = false, bool WT = false, bool LOOPED = false, bool IPN = false>
+          int FSM = 0, bool SHTW = false, bool WT = false, bool LOOPED = false, int IPN = 0>
 __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                           const PassArgs<E>& A, const uint32_t w, const uint32_t bq,
                                           uint32_t* __restrict__ lds, uint32_t* __restrict__ lds_tw) {
@@ -598,7 +626,7 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
     }
   }
 
-  if constexpr (IPN) ipn_signal_read(A, mid);  // this tile's elements are in registers now
+  if constexpr (IPN == 1) ipn_signal_read(A, mid);  // this tile's elements are in registers now
 
   // ------------------------------------------------------------------ sub-stages 1..nsub-1 via LDS
   if constexpr (S::nsub > 1) substage<E, LOGR, T, TE, NT, 1, FAST, R32, LTW>(x, cl, pil, lds, A, t, lds_tw, w);
@@ -609,8 +637,10 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
   static_assert(S::nsub <= 6, "sub-stages");
 
   // ------------------------------------------------------------------ output
-  if constexpr (IPN) {  // the slab this tile writes into has been read (or the wait gave up: no stores)
+  if constexpr (IPN == 1) {  // the slab this tile writes into has been read (or the wait gave up: no stores)
     if (!ipn_wait_mirror(A, midrev)) return;
+  } else if constexpr (IPN == 2) {  // in-place single launch: every final tile has read (grid barrier)
+    if (!ipn_grid_barrier(A)) return;
   }
 #if NTT_PRIO & 2
   __builtin_amdgcn_s_setprio(1);  // timing experiment: finishing tiles drain first
@@ -748,14 +778,14 @@ void k_final_ipn(uint32_t* data, const PassArgs<E> A) {
   const uint32_t w = s_w;
   if constexpr (E::FASTRED) {
     if (A.F.red_ok)
-      pass_tile<E, LOGR, KIND_FINAL, false, true, PRO_NONE, true, 0, false, false, false, true>(data, data, A, w, 0, lds,
-                                                                                              lds_tw);
+      pass_tile<E, LOGR, KIND_FINAL, false, true, PRO_NONE, true, 0, false, false, false, 1>(data, data, A, w, 0, lds,
+                                                                                           lds_tw);
     else
-      pass_tile<E, LOGR, KIND_FINAL, false, false, PRO_NONE, true, 0, false, false, false, true>(data, data, A, w, 0,
-                                                                                               lds, lds_tw);
+      pass_tile<E, LOGR, KIND_FINAL, false, false, PRO_NONE, true, 0, false, false, false, 1>(data, data, A, w, 0,
+                                                                                            lds, lds_tw);
   } else {
-    pass_tile<E, LOGR, KIND_FINAL, false, false, PRO_NONE, true, 0, false, false, false, true>(data, data, A, w, 0, lds,
-                                                                                             lds_tw);
+    pass_tile<E, LOGR, KIND_FINAL, false, false, PRO_NONE, true, 0, false, false, false, 1>(data, data, A, w, 0, lds,
+                                                                                          lds_tw);
   }
   if (t == 0)
     s_last = __hip_atomic_fetch_add(A.ipn_sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
@@ -766,7 +796,10 @@ void k_final_ipn(uint32_t* data, const PassArgs<E> A) {
       A.ipn_sync[32 * (1 + m)] = 0u;
       A.ipn_sync[32 * (1 + m) + 1] = 0u;
     }
-    if (t == 0) A.ipn_sync[0] = A.ipn_sync[1] = A.ipn_sync[2] = 0u;
+    if (t == 0) {
+      A.ipn_sync[0] = A.ipn_sync[1] = 0u;
+      if (A.wd.abort) *A.wd.abort = 0u;
+    }
   }
 }
 
@@ -861,12 +894,12 @@ __device__ __forceinline__ bool fused_wait(uint32_t* ready, const FusedArgs& F) 
   if (F.dbg & 1u) return true;  // diagnostics only: no dependency waits (wrong output)
   __shared__ uint32_t s_ok;
   if (threadIdx.x == 0) {
-    s_ok = poll_bounded<2, 4, 8, 16, 32>(ready, F.sync + 2, F.wd) ? 1u : 0u;
+    s_ok = poll_bounded<2, 4, 8, 16, 32>(ready, F.wd) ? 1u : 0u;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  return s_ok != 0u;
+  return __builtin_amdgcn_readfirstlane(s_ok) != 0u;
 }
 
 template <class E>
@@ -957,6 +990,7 @@ void k_fused3(const FusedKArgs<E> K) {
     // the last workgroup out: nobody touches the counters again in this launch
     const uint32_t words = F.rbase + 32 * (F.n12 + F.n23);
     for (uint32_t i = 0; i < words; ++i) __hip_atomic_store(F.sync + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (F.wd.abort) __hip_atomic_store(F.wd.abort, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -975,20 +1009,7 @@ void k_fused3(const FusedKArgs<E> K) {
 // re-zeroes the words for the next launch.
 // False (workgroup-uniform) when the wait gave up (Watchdog): the workgroup then skips the passes left.
 __device__ __forceinline__ bool fused_grid_barrier(const FusedArgs& F, uint32_t k) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores are done
-  __syncthreads();
-  __shared__ uint32_t s_ok;
-  uint32_t* const go = F.sync + F.rbase + 32 * (k - 1);
-  if (threadIdx.x == 0) {
-    if (__hip_atomic_fetch_add(F.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k * gridDim.x - 1)
-      __hip_atomic_store(go, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // poll the go word with relaxed agent-scope loads (global, not flat), bounded like fused_wait
-    s_ok = poll_bounded<4, 16, 32, 16, 32>(go, F.sync + 2, F.wd) ? 1u : 0u;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  return s_ok != 0u;
+  return grid_barrier_words(F.sync, F.sync + F.rbase + 32 * (k - 1), k * gridDim.x, F.wd);
 }
 
 template <class E, int R1, int R2, int R3>
@@ -1025,9 +1046,55 @@ void k_fused3b(const FusedKArgs<E> K) {
     // the last workgroup out: every other one has passed both barriers
     __hip_atomic_store(F.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(F.sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(F.sync + 2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (F.wd.abort) __hip_atomic_store(F.wd.abort, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(F.sync + F.rbase, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(F.sync + F.rbase + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// The single-launch schedule of an NTT_PLAN_IN_PLACE plan (FusedArgs::mode 2; BASELINE config 2's
+// "single-kernel self-sort-in-place"): no scratch, every pass in the caller's buffer.  Passes 1 and 2
+// write the positions they read (write-through, as k_fused3b); the final pass of the palindromic
+// schedule writes its outputs to their natural positions, which lie in the mirror slab, so every final
+// tile loads and transforms, a third grid barrier makes sure every tile has read, and only then do the
+// tiles store (IPN = 2 in pass_tile).  That needs every final tile resident at once: one tile per
+// workgroup, nwg == tiles (n <= 2^20 at 4 workgroups per CU), a cooperative launch.
+template <class E, int R1, int R2, int R3>
+__global__ __launch_bounds__((1 << E::TILE_LOG) / E::EPT) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
+void k_fused3bi(const FusedKArgs<E> K) {
+  static_assert(E::FASTRED && E::SHOUP_OUTER && !E::LDS_TW && E::SCRW == E::MEMW, "fused in place: 256-bit engines");
+  constexpr int LW = pass_lds_words<E, R1, KIND_COLUMN>();
+  static_assert(LW == pass_lds_words<E, R3, KIND_FINAL>(), "one tile size");
+  __shared__ __attribute__((aligned(16))) uint32_t lds[LW];
+  __shared__ uint32_t lds_tw[1];
+  const FusedArgs& F = K.F;
+  const uint32_t G = gridDim.x;
+  for (uint32_t w = blockIdx.x; w < F.tiles; w += G) {  // pass 1, in place
+    const FusedKArgs<E>& L = fused_kargs<E>();
+    pass_tile<E, R1, KIND_COLUMN, true, true, PRO_NONE, true, 0, false, true, true>(L.dst, L.dst, L.A1, w, 0, lds,
+                                                                                      lds_tw);
+    __syncthreads();
+  }
+  bool ok = fused_grid_barrier(F, 1);
+  for (uint32_t w = blockIdx.x; ok && w < F.tiles; w += G) {  // pass 2, in place
+    const FusedKArgs<E>& L = fused_kargs<E>();
+    pass_tile<E, R2, KIND_COLUMN, true, true, PRO_NONE, true, 0, true, true, true>(L.dst, L.dst, L.A2, w, 0, lds,
+                                                                                     lds_tw);
+    __syncthreads();
+  }
+  ok = ok && fused_grid_barrier(F, 2);
+  if (ok && blockIdx.x < F.tiles) {  // final pass: load, transform, barrier 3 (inside), natural-order stores
+    const FusedKArgs<E>& L = fused_kargs<E>();
+    pass_tile<E, R3, KIND_FINAL, false, true, PRO_NONE, true, 0, false, false, true, 2>(L.dst, L.dst, L.A3,
+                                                                                         blockIdx.x, 0, lds, lds_tw);
+  }
+  if (threadIdx.x == 0 && __hip_atomic_fetch_add(F.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
+    // the last workgroup out: every other one has passed (or given up at) all three barriers
+    __hip_atomic_store(F.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(F.sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (F.wd.abort) __hip_atomic_store(F.wd.abort, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t k = 0; k < 3; ++k)
+      __hip_atomic_store(F.sync + F.rbase + 32 * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1046,6 +1113,16 @@ hipError_t launch_fused3(int r1, int r2, int r3, const uint32_t* src, uint32_t* 
       return !(v && *v == '0');
     }();
     // mode 1: a cooperative launch (every workgroup resident, or the launch fails: never a hang)
+    if (F.mode == 2) {  // in place: cooperative launch of exactly one workgroup per tile
+#define NTT_FUSED_IP_CASE(a, c, d)                                                                \
+  if (r1 == a && r2 == c && r3 == d)                                                              \
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_fused3bi<E, a, c, d>), g, b, kargs, 0, st);
+      NTT_FUSED_IP_CASE(6, 6, 6)
+      NTT_FUSED_IP_CASE(6, 7, 6)
+      NTT_FUSED_IP_CASE(7, 6, 7)
+#undef NTT_FUSED_IP_CASE
+      return hipErrorInvalidValue;
+    }
 #define NTT_FUSED_CASE(a, c, d)                                                                   \
   if (r1 == a && r2 == c && r3 == d) {                                                            \
     if (F.mode == 1 && coop)                                                                      \
@@ -1084,6 +1161,15 @@ hipError_t fused3_capacity(int r1, int r2, int r3, int device, uint32_t* wgs, ui
         &per, mode == 1 ? reinterpret_cast<const void*>(&k_fused3b<E, a, c, d>)                        \
                         : reinterpret_cast<const void*>(&k_fused3<E, a, c, d>),                        \
         threads, 0);
+#define NTT_FUSED_IP_OCC(a, c, d)                                                                      \
+  if (mode == 2 && r1 == a && r2 == c && r3 == d)                                                      \
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&k_fused3bi<E, a, c, d>), \
+                                                     threads, 0);
+    NTT_FUSED_IP_OCC(6, 6, 6)
+    NTT_FUSED_IP_OCC(6, 7, 6)
+    NTT_FUSED_IP_OCC(7, 6, 7)
+#undef NTT_FUSED_IP_OCC
+    if (mode != 2) {
     NTT_FUSED_OCC(6, 6, 6)
     NTT_FUSED_OCC(7, 6, 6)
     NTT_FUSED_OCC(7, 7, 6)
@@ -1091,6 +1177,7 @@ hipError_t fused3_capacity(int r1, int r2, int r3, int device, uint32_t* wgs, ui
     NTT_FUSED_OCC(8, 7, 7)
     NTT_FUSED_OCC(8, 8, 7)
     NTT_FUSED_OCC(8, 8, 8)
+    }
 #undef NTT_FUSED_OCC
     if (e != hipSuccess) return e;
     *wgs = (uint32_t)(cus * per);

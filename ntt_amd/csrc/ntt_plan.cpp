@@ -80,6 +80,36 @@ static bool vec_lt(const Vec<N>& a, const Vec<N>& b) {
   return false;
 }
 
+// ------------------------------------------------------------------------------ watchdog words
+// One 4-KiB mapped, coherent pinned page per 1024 plans that use inter-workgroup waits; a plan takes
+// a 4-byte slot when it first builds such a schedule and returns it when destroyed.  The pages are
+// never freed: nothing is released during process teardown, where the HIP runtime (and a profiler
+// such as rocprofv3) may already be gone.
+static std::mutex g_watch_mu;
+static std::vector<uint32_t*> g_watch_free;
+static uint32_t* watch_slot_acquire() {
+  std::lock_guard<std::mutex> lk(g_watch_mu);
+  if (g_watch_free.empty()) {
+    void* page = nullptr;
+    if (hipHostMalloc(&page, 4096, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess)
+      return nullptr;
+    auto* w = static_cast<uint32_t*>(page);
+    for (int i = 1023; i >= 0; --i) {
+      w[i] = 0u;
+      g_watch_free.push_back(w + i);
+    }
+  }
+  uint32_t* s = g_watch_free.back();
+  g_watch_free.pop_back();
+  *s = 0u;
+  return s;
+}
+static void watch_slot_release(uint32_t* s) {
+  if (!s) return;
+  std::lock_guard<std::mutex> lk(g_watch_mu);
+  g_watch_free.push_back(s);
+}
+
 // ------------------------------------------------------------------------------ plan
 struct PlanBase {
   virtual ~PlanBase() = default;
@@ -117,23 +147,17 @@ struct PlanBase {
   // Watchdog report (ntt_kernels.hpp): a host-mapped word that a kernel sets when one of its bounded
   // inter-workgroup waits gives up.  Every later call on the plan returns NTT_ERR_DEVICE (a plain host
   // read, no device query) until ntt_plan_device_status reads and clears it.
-  uint32_t* h_watch = nullptr;  // host pointer (hipHostMalloc, mapped, coherent)
+  // The word is a slot of a process-wide pinned page (watch_slot_acquire below), taken when the plan
+  // first builds a schedule with such waits; plans that never do hold none.
+  uint32_t* h_watch = nullptr;  // host pointer (a slot of the mapped, coherent page)
   uint32_t* d_watch = nullptr;  // its device alias (the kernels' Watchdog::report)
   uint32_t wd_spins = 1u << 21; // poll limit of a wait (~2 s); ntt_plan_set_watchdog
   bool tripped() const { return h_watch && __atomic_load_n(h_watch, __ATOMIC_ACQUIRE) != 0u; }
   void clear_trip() {
     if (h_watch) __atomic_store_n(h_watch, 0u, __ATOMIC_RELEASE);
   }
-  ntt::Watchdog watchdog() const { return ntt::Watchdog{d_watch, wd_spins}; }
-  int alloc_watch() {
-    if (hipHostMalloc(reinterpret_cast<void**>(&h_watch), 4, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
-      h_watch = nullptr;
-      return NTT_ERR_HIP;
-    }
-    *h_watch = 0u;
-    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d_watch), h_watch, 0) != hipSuccess) return NTT_ERR_HIP;
-    return NTT_OK;
-  }
+  ntt::Watchdog watchdog(uint32_t* abort_w) const { return ntt::Watchdog{d_watch, abort_w, wd_spins}; }
+  bool alloc_watch();  // true once the plan holds a report word (defined after the slot pool)
   void begin(hipStream_t st) {
     if (!profiling) return;
     slot = nrec % kSlots;
@@ -145,6 +169,20 @@ struct PlanBase {
     if (profiling && ev_used < kEv) (void)hipEventRecord(ev[slot][ev_used++], st);
   }
 };
+
+bool PlanBase::alloc_watch() {
+  if (h_watch) return true;
+  h_watch = watch_slot_acquire();
+  if (!h_watch) return false;
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h_watch, 0) != hipSuccess) {
+    watch_slot_release(h_watch);
+    h_watch = nullptr;
+    return false;
+  }
+  d_watch = static_cast<uint32_t*>(d);
+  return true;
+}
 
 // radices for log_n: near-equal split with each radix <= tile_log - min_cols_log so that every
 // global access is a contiguous run of T = TILE / R >= 2^min_cols_log elements (>= 128 B).
@@ -433,10 +471,11 @@ struct PlanImpl final : PlanBase {
     if (d_coset) (void)hipFree(d_coset);
     if (d_coset_full) (void)hipFree(d_coset_full);
     if (d_sync) (void)hipFree(d_sync);
+    if (d_sync_ip) (void)hipFree(d_sync_ip);
     if (d_ipn) (void)hipFree(d_ipn);
     if (d_pw) (void)hipFree(d_pw);
     if (d_dbg) (void)hipFree(d_dbg);
-    if (h_watch) (void)hipHostFree(h_watch);
+    watch_slot_release(h_watch);
     for (auto& row : ev)
       for (auto& e : row)
         if (e) (void)hipEventDestroy(e);
@@ -612,7 +651,6 @@ struct PlanImpl final : PlanBase {
     if (hipMalloc(&d_tab, host.size() * 4) != hipSuccess ||
         hipMemcpy(d_tab, host.data(), host.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
       rc = NTT_ERR_HIP;
-    if (rc == NTT_OK) rc = alloc_watch();
 #if NTT_DEBUG_CHECKS
     // debug builds: the status word every kernel of this plan records check failures in
     if (rc == NTT_OK && (hipMalloc(&d_dbg, 4) != hipSuccess || hipMemset(d_dbg, 0, 4) != hipSuccess)) rc = NTT_ERR_HIP;
@@ -1121,8 +1159,24 @@ struct PlanImpl final : PlanBase {
         if (!io && !inplace && batch == 1 && fused_enabled() && fused_ready(PA)) {
           // one persistent launch for the three passes (NTT_PLAN_SINGLE_LAUNCH, k_fused3)
           FusedArgs F = fused_args();
-          F.wd = watchdog();
+          F.wd = watchdog(F.wd.abort);
           e = launch_fused3<E>((int)r[0], (int)r[1], (int)r[2], in, work, out, PA[0], PA[1], PA[2], F, st);
+          mark(st);
+          return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+        }
+      }
+      if constexpr (std::is_same_v<E, Eng256>) {
+        if (!io && inplace && batch == 1 && fused_enabled() && fused_ip_ready(PA)) {
+          // the in-place single launch (k_fused3bi): three passes in the caller's buffer, no scratch
+          FusedArgs F = fargs_ip;
+          F.wd = watchdog(F.wd.abort);
+          PassArgs<E> B = A;
+          B.flags &= ~2u;
+          B.ipn_sync = F.sync;
+          B.ipn_go = F.sync + F.rbase + 64;  // the third barrier's go word
+          B.ipn_strips = 3 * F.nwg;          // its arrival target (the counter is cumulative)
+          B.wd = F.wd;
+          e = launch_fused3<E>((int)r[0], (int)r[1], (int)r[2], out, nullptr, out, PA[0], PA[1], B, F, st);
           mark(st);
           return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
         }
@@ -1137,9 +1191,9 @@ struct PlanImpl final : PlanBase {
         PassArgs<E> B = A;
         B.flags &= ~2u;
         B.ipn_sync = d_ipn;
-        B.ipn_order = d_ipn + 32 * (1 + ipn_slabs);
+        B.ipn_order = d_ipn + 32 * (2 + ipn_slabs);
         B.ipn_strips = ipn_strips;
-        B.wd = watchdog();
+        B.wd = watchdog(d_ipn + 32 * (1 + ipn_slabs));
         e = launch_final_ipn<E>((int)r[npass - 1], out, B, grid, st);
         mark(st);
       } else if (e == hipSuccess) {
@@ -1192,6 +1246,7 @@ struct PlanImpl final : PlanBase {
       return false;
     } else {
     if (npass != 3 || !use_full || !d_full_sh || !full_sh_ok[1] || !Ff.red_ok) return false;
+    if (!alloc_watch()) return false;
     const unsigned tl = tile_log_of<E>();
     // NTT_FUSED_MODE=0: the dataflow form (per-tile hand-offs), =1: the grid-barrier form (default);
     // read when the plan builds its fused schedule (its first single-launch call)
@@ -1221,18 +1276,59 @@ struct PlanImpl final : PlanBase {
               F.nwg, cap);
     if (const char* v = getenv("NTT_FUSED_DBG")) F.dbg = (uint32_t)atoi(v);
     F.rbase = (4 + F.n12 + F.n23 + 31) & ~31u;
-    const size_t words = F.rbase + 32 * (F.n12 + F.n23);
-    if (hipMalloc(&d_sync, words * 4) != hipSuccess) {
+    const size_t words = F.rbase + 32 * (F.n12 + F.n23);  // then the abort word on a line of its own
+    if (hipMalloc(&d_sync, (words + 32) * 4) != hipSuccess) {
       d_sync = nullptr;
       return false;
     }
-    if (hipMemset(d_sync, 0, words * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return false;
+    if (hipMemset(d_sync, 0, (words + 32) * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return false;
     F.sync = d_sync;
+    F.wd.abort = d_sync + words;
     fargs = F;
     return true;
     }
   }
   const FusedArgs& fused_args() const { return fargs; }
+
+  // ---- the in-place single launch (NTT_PLAN_SINGLE_LAUNCH on an NTT_PLAN_IN_PLACE plan, k_fused3bi):
+  // 3-pass palindromic FAST 256-bit schedules whose tiles all fit the device at once (2^18 .. 2^20)
+  uint32_t* d_sync_ip = nullptr;  // [0] arrivals, [1] exits; go words at 32, 64, 96; abort at 128
+  FusedArgs fargs_ip{};
+  bool fused_ip_built = false, fused_ip_ok = false;
+  bool fused_ip_ready(const PassArgs<E>* PA) {
+    if (!fused_ip_built) {
+      fused_ip_built = true;
+      fused_ip_ok = build_fused_ip();
+    }
+    return fused_ip_ok && PA[0].tw_full && PA[1].tw_full && PA[1].tw_sh && !PA[0].src2 && !PA[0].tw_in;
+  }
+  bool build_fused_ip() {
+    if constexpr (!std::is_same_v<E, Eng256>) {
+      return false;
+    } else {
+      if (npass != 3 || r[0] != r[2] || !use_full || !d_full_sh || !full_sh_ok[1] || !Ff.red_ok) return false;
+      if (!alloc_watch()) return false;
+      const uint32_t tiles = (uint32_t)(n >> tile_log_of<E>());
+      uint32_t cap = 0;
+      if (fused3_capacity<E>((int)r[0], (int)r[1], (int)r[2], device, &cap, 2) != hipSuccess || cap < tiles) return false;
+      FusedArgs F{};
+      F.tiles = F.nwg = tiles;
+      F.mode = 2;
+      F.rbase = 32;
+      if (const char* v = getenv("NTT_FUSED_VERBOSE"))
+        fprintf(stderr, "libntt: in-place single launch, %u tiles per pass, %u workgroups (capacity %u)\n", tiles,
+                tiles, cap);
+      if (hipMalloc(&d_sync_ip, 160 * 4) != hipSuccess) {  // go words at 32, 64, 96; abort at 128
+        d_sync_ip = nullptr;
+        return false;
+      }
+      if (hipMemset(d_sync_ip, 0, 160 * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return false;
+      F.sync = d_sync_ip;
+      F.wd.abort = d_sync_ip + 128;
+      fargs_ip = F;
+      return true;
+    }
+  }
   // bit 0: a bounded wait gave up (the watchdog report, PlanBase::h_watch); then cleared.  Blocking:
   // the device is synchronised first, so the report covers every call enqueued before.
   int device_status(unsigned* bad) override {
@@ -1266,6 +1362,7 @@ struct PlanImpl final : PlanBase {
   bool build_ipn(const PassArgs<E>& A) {
     const unsigned tl = tile_log_of<E>(), rp = r[npass - 1];
     if (npass < 2 || r[0] != rp || rp > 9 || tl < rp) return false;
+    if (!alloc_watch()) return false;
     const unsigned mid_log = log_n - r[0] - rp;
     ipn_slabs = 1u << mid_log;
     ipn_strips = 1u << (r[0] - (tl - rp));  // R_1 / T, T = TILE / R_p
@@ -1294,7 +1391,7 @@ struct PlanImpl final : PlanBase {
         seen[q] = 1;
       }
     }
-    const size_t sync_words = 32 * (1 + (size_t)ipn_slabs);
+    const size_t sync_words = 32 * (2 + (size_t)ipn_slabs);  // line 0, one line per slab, the abort line
     if (hipMalloc(&d_ipn, (sync_words + order.size()) * 4) != hipSuccess) {
       d_ipn = nullptr;
       return false;
@@ -1750,9 +1847,10 @@ struct CachedPlan {
 };
 }  // namespace
 static std::mutex g_cache_mu;
-static std::map<std::tuple<std::vector<uint64_t>, std::vector<uint64_t>, unsigned, unsigned, int>,
-                std::shared_ptr<CachedPlan>>
-    g_cache;
+// Heap-held and never destroyed: cached plans outliving main() are not torn down after the HIP runtime
+// (static destructors run in an unspecified order relative to it); ntt_shim_cache_clear frees them.
+static auto& g_cache = *new std::map<std::tuple<std::vector<uint64_t>, std::vector<uint64_t>, unsigned, unsigned, int>,
+                                     std::shared_ptr<CachedPlan>>();
 static uint64_t g_cache_tick = 0;
 // At most NTT_SHIM_CACHE_PLANS (default 8) cached plans; the least recently used one is dropped
 // when a new key arrives (a call still running on it keeps it alive through its shared_ptr).

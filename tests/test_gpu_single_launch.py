@@ -105,3 +105,61 @@ def test_single_launch_edges_and_interleaving():
         fused.forward(b)
         assert torch.equal(a, b), name
     assert fused.device_status() == 0
+
+
+# ---- the in-place single launch (BASELINE C2's "single-kernel self-sort-in-place")
+def _ip_plan(fid, log_n, single=True):
+    from ntt_amd.ntt import NTTPlan
+    return NTTPlan(field_id=fid, log_n=log_n, limbs64=4, device=0, single_launch=single, in_place=True)
+
+
+@pytest.mark.parametrize("kind", ["iota", "random"])
+def test_c2_2pow20_in_place_single_launch_vs_oracle(kind):
+    """2^20 BN254 as ONE kernel with no scratch (k_fused3bi): passes 1 and 2 in place, the final pass's
+    digit reversal behind a third grid barrier.  Bit for bit against the threaded C oracle (forward and
+    inverse), the KAT of x_j = j, exactly one launch, and no plan buffer."""
+    fid, log_n = 1, 20
+    p, g = R.FIELDS[fid]
+    pl = _ip_plan(fid, log_n)
+    assert pl.passes == [7, 6, 7]
+    t = pl.fill(pl.empty(), kind, seed=2)
+    x = _host(t).copy()
+    pl.set_profiling(True)
+    pl.forward(t)
+    launches = pl.last_launch_ms()
+    pl.set_profiling(False)
+    assert len(launches) == 1, launches
+    assert np.array_equal(_host(t), OC.ntt_mp_par(x, p, g, THREADS))
+    if kind == "iota":
+        n = 1 << log_n
+        got = _host(t)
+        for k in (0, 1, 2, n // 2, n - 1):
+            assert OC.limbs_to_ints(got[k:k + 1])[0] == R.kat_xj(n, p, g, k)
+    t.copy_(torch.from_numpy(x.view(np.int64)).to(t.device))
+    pl.inverse(t)
+    assert np.array_equal(_host(t), OC.ntt_mp_par(x, p, g, THREADS, inverse=True))
+    assert pl.device_status() == 0
+
+
+@pytest.mark.parametrize("fid", [1, 2])
+@pytest.mark.parametrize("log_n", [18, 19, 20, 21])
+def test_in_place_single_launch_matches_default(fid, log_n):
+    """2^18..2^20 run as one launch (every final tile resident); 2^21 has more tiles than the device
+    keeps resident and falls back to the in-place multi-launch schedule.  Both equal the default plan,
+    over repeated calls (the barrier words re-arm) and the round trip."""
+    ip = _ip_plan(fid, log_n)
+    df = _plan(fid, log_n, False)
+    for seed in (1, 2, 3):
+        a = ip.fill(ip.empty(), "random", seed=seed)
+        b = a.clone()
+        x = a.clone()
+        ip.set_profiling(True)
+        ip.forward(a)
+        nl = len(ip.last_launch_ms())
+        ip.set_profiling(False)
+        df.forward(b)
+        assert torch.equal(a, b), (fid, log_n, seed)
+        assert nl == (1 if log_n <= 20 else 3), nl
+        ip.inverse(a)
+        assert torch.equal(a, x)
+    assert ip.device_status() == 0

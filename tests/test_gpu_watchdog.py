@@ -22,14 +22,16 @@ def _fresh(plan, seed):
 
 @pytest.mark.parametrize("flag,log_n,direction", [("in_place", 22, "forward"), ("in_place", 22, "inverse"),
                                                    ("in_place", 20, "forward"), ("single", 20, "forward"),
-                                                   ("single", 20, "inverse"), ("dataflow", 20, "forward")])
+                                                   ("single", 20, "inverse"), ("dataflow", 20, "forward"),
+                                                   ("ip_single", 20, "forward"), ("ip_single", 19, "inverse")])
 def test_watchdog_trip_is_reported_and_plan_recovers(flag, log_n, direction, monkeypatch):
     from ntt_amd import lib as L
     from ntt_amd.ntt import NTTPlan
-    if flag != "in_place":  # the single-launch form: grid barriers (1, default) or dataflow hand-offs (0)
+    if flag in ("single", "dataflow"):  # the single-launch form: grid barriers (1, default) or dataflow (0)
         monkeypatch.setenv("NTT_FUSED_MODE", "1" if flag == "single" else "0")
     ref = NTTPlan(1, log_n, 4)
-    pl = NTTPlan(1, log_n, 4, in_place=flag == "in_place", single_launch=flag != "in_place")
+    # ip_single: the in-place single launch (three grid barriers, k_fused3bi)
+    pl = NTTPlan(1, log_n, 4, in_place=flag in ("in_place", "ip_single"), single_launch=flag != "in_place")
     run = (lambda p, t: p.forward(t)) if direction == "forward" else (lambda p, t: p.inverse(t))
     x = _fresh(ref, 3)
     want = x.clone()

@@ -18,6 +18,7 @@ PYT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
 for s in "$@"; do
   case $s in
     new) step pytest_new 400 $PYT tests/test_gpu_mplan_copy.py tests/test_gpu_watchdog.py ;;
+    sl) step pytest_sl 600 $PYT tests/test_gpu_single_launch.py tests/test_gpu_inplace.py tests/test_gpu_watchdog.py ;;
     dist) step pytest_dist 600 $PYT tests/test_gpu_distributed.py tests/test_gpu_polymul_dist.py tests/test_gpu_mplan_faults.py tests/test_gpu_mplan_copy.py ;;
     tests) step pytest_gpu 1100 $PYT tests -m gpu ;;
     smoke) step smoke 120 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
@@ -26,6 +27,10 @@ for s in "$@"; do
     bench) step bench 300 python3 -u bench.py ;;
     benchd) step bench_driver 300 python3 -u bench.py --steps 20 --warmup 5 ;;
     fs1) step bench_fourstep_w1 300 python3 -u bench.py --four-step --steps 20 --warmup 10 --no-cpu-baseline ;;
+    profd) step rocprof_driver 300 rocprofv3 --kernel-trace --stats -d $O/profd -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    prof_plain) step rocprof_plain 200 rocprofv3 --kernel-trace --stats -d $O/prof_plain -o run --output-format csv -- python3 tools/exp_launches.py --cfg f1_L4_n20 --warmup 5 --steps 10 ;;
+    prof_ip) step rocprof_ip 200 rocprofv3 --kernel-trace --stats -d $O/prof_ip -o run --output-format csv -- python3 tools/exp_launches.py --cfg f1_L4_n20_ip --warmup 5 --steps 10 ;;
+    prof_sl) step rocprof_sl 200 rocprofv3 --kernel-trace --stats -d $O/prof_sl -o run --output-format csv -- python3 tools/exp_launches.py --cfg f1_L4_n20_sl --warmup 5 --steps 10 ;;
     prof) step rocprof_stats 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py ;;
     pmc)
       step pmc_sq 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d $O/pmc/sq -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity
@@ -36,6 +41,16 @@ for s in "$@"; do
       step limb30_prep 60 python tools/mb_limb30_check.py prep $O/limb30
       step limb30_run 300 tools/mb_limb30 $O/limb30/consts.bin $O/limb30/xs.bin $O/limb30/rs.bin
       step limb30_verify 120 python tools/mb_limb30_check.py verify $O/limb30 ;;
+    c2)  # BASELINE C2 (2^20 BN254) forms: 3 launches, single launch (barriers / dataflow), in place, in place as one kernel
+      L="--warmup 50 --steps 200"
+      C="--cfg f1_L4_n20 --cfg f1_L4_n20_sl --cfg f1_L4_n20_ip --cfg f1_L4_n20_ip_sl --cfg f1_L4_n19_ip_sl --cfg f1_L4_n18_ip_sl --cfg f1_L4_n18_sl"
+      for rep in 1 2; do
+        step c2_ab_m1_$rep 200 python -u tools/exp_launches.py $C $L
+        cat $O/c2_ab_m1_$rep.log | grep '^{' | sed "s/^/mode1 /" >> $O/c2_ab.txt
+        step c2_ab_m0_$rep 200 env NTT_FUSED_MODE=0 python -u tools/exp_launches.py --cfg f1_L4_n20_sl $L
+        cat $O/c2_ab_m0_$rep.log | grep '^{' | sed "s/^/mode0 /" >> $O/c2_ab.txt
+      done
+      step c2_prof 300 rocprofv3 --kernel-trace --stats -d $O/c2prof -o run --output-format csv -- python3 tools/exp_launches.py $C --warmup 20 --steps 100 ;;
     configs) step configs 600 python -u tools/bench_configs.py --out $O/configs.jsonl ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
   esac
