@@ -354,7 +354,9 @@ def secondary_timings(args, eng, dist, rccl, local, barrier):
     L = eng.layout
     ar = DistNTT.auto_pieces(L.local_n)
     ac = DistNTT.auto_pieces(L.local_n, cap=4, min_elems=DistNTT.MIN_COL_PIECE_ELEMS)
-    if (ar, ac) != (len(eng.fs.pieces), eng.fs.cp):
+    if getattr(args, "_tuned", False):
+        res["pipelined_pieces"] = {"skipped": "timed by the exchange-schedule measurement (exchange_schedule)"}
+    elif (ar, ac) != (len(eng.fs.pieces), eng.fs.cp):
         e2 = DistNTT(field_id=args.field, log_n=args.log_n, limbs64=args.limbs, device=local,
                      host_exchange=not rccl, pieces="auto", col_pieces="auto")
         d2 = e2.empty()
@@ -419,10 +421,15 @@ def main():
         eng = DistNTT(field_id=args.field, log_n=args.log_n, limbs64=args.limbs, device=local,
                       host_exchange=rehearsal, pieces=args.pieces, col_pieces=args.col_pieces)
         data = eng.empty()
+        tuned = None
+        if world > 1 and args.pieces is None and args.col_pieces is None:
+            # the exchange schedule is chosen by measurement on this node (DistNTT.tune_pieces)
+            tuned = eng.tune_pieces(data if not args.inverse else eng.empty())
         eng.fill(data, "random", seed=2)
         step = (lambda: eng.inverse(data)) if args.inverse else (lambda: eng.forward(data))
         plan_for_prof = eng
     else:
+        tuned = None
         from ntt_amd.ntt import NTTPlan
         plan = NTTPlan(field_id=args.field, log_n=args.log_n, limbs64=args.limbs, device=local)
         data = plan.empty()
@@ -517,6 +524,9 @@ def main():
         # world size of the RCCL (nccl-backend) process group carrying the data path; 0 = none
         "rccl_ranks": world if rccl else 0,
     }
+    if four_step and tuned is not None:
+        out["exchange_schedule"] = {**tuned, "how": "measured before the warmup: each candidate's forward "
+                                    "timed on every rank (max over ranks), the fastest kept for the timed steps"}
     if four_step:
         # rank 0's all-to-all window per transform (HIP events on the compute stream around the
         # exchange: from the first piece's start to the last piece's arrival; with the default single
@@ -579,6 +589,7 @@ def main():
     # pipelined exchange pieces (opt-in until they measurably win) and one independent transform per
     # rank (weak scaling, no data-path collective)
     if four_step and world > 1 and not args.no_secondary:
+        args._tuned = tuned is not None
         sec = secondary_timings(args, eng, dist, rccl, local, barrier)
         if rank == 0:
             out["secondary"] = sec

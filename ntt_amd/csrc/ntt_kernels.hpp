@@ -123,7 +123,7 @@ struct PassArgs {
   const uint32_t* ipn_order; // slab (middle-digit value) of the i-th slab in ticket order (pairs adjacent)
   uint32_t ipn_strips;       // workgroups per slab (R_1 / T)
   uint32_t* ipn_go;          // k_fused3bi (the in-place single launch): the final pass's barrier go word
-                             // (ipn_sync: the launch's sync words, ipn_strips: that barrier's arrival target)
+  uint32_t* ipn_shards;      //   and its arrival shard lines (ipn_sync: the top counter)
   Watchdog wd;               // bounded waits (k_final_ipn, k_fused3bi)
   // debug builds (NTT_DEBUG_CHECKS): element extents of src / dst from this transform's first element
   // (~0: not checked, e.g. four-step maps into the caller's exchange blocks)
@@ -154,7 +154,8 @@ struct FusedArgs {
   uint32_t mode;               // 0: dataflow hand-offs between tiles (k_fused3); 1: two grid barriers
                                // over a cooperative launch (k_fused3b); 2: the NTT_PLAN_IN_PLACE form,
                                // three grid barriers, one workgroup per tile (k_fused3bi)
-  Watchdog wd;                 // bounded waits; sync[2] is the launch's abort word
+  Watchdog wd;                 // bounded waits
+  uint32_t* shards;            // grid barriers (modes 1, 2): 8 arrival shards, one 128-B line each
 };
 template <class E>
 hipError_t launch_fused3(int r1, int r2, int r3, const uint32_t* src, uint32_t* scratch, uint32_t* dst,

@@ -363,18 +363,27 @@ __device__ __forceinline__ bool ipn_wait_mirror(const PassArgs<E>& A, uint32_t m
   return __builtin_amdgcn_readfirstlane(s_ok) != 0u;  // wave-uniform: scalar branches around it
 }
 
-// Grid-wide barrier over a cumulative arrival counter (barrier k of a launch completes at k G
-// arrivals), the guide's R1 publish (MI355X_MICROARCH.md § visibility): every wave drains its
-// (write-through) stores, a workgroup barrier, one lane's agent-scope add; the last arrival raises the
-// barrier's go word (a 128-B line of its own); one lane polls it (bounded, Watchdog), ONE agent-scope
-// acquire, and the workgroup barrier releases every wave.  False (workgroup-uniform) when the wait
-// gave up: the workgroup then skips what is left of the launch.
-__device__ __forceinline__ bool grid_barrier_words(uint32_t* counter, uint32_t* go, uint32_t target, const Watchdog& wd) {
+// Grid-wide barrier k of a launch (k = 1, 2, ...), the guide's R1 publish (MI355X_MICROARCH.md
+// § visibility): every wave drains its (write-through) stores, a workgroup barrier, then one lane's
+// agent-scope add.  The arrivals are sharded: workgroup b adds to shard b mod 8 (8 counters, each on a
+// 128-B line of its own, cumulative: shard s completes barrier k at k n_s arrivals, n_s = its
+// workgroups), and the last arrival of each shard adds to the top counter, whose last arrival (k S,
+// S = non-empty shards) raises the barrier's go word.  One counter taking all G arrivals serialises
+// them (the guide's fan-in: ~12 ns per atomic, ~12 us at G = 1024); eight shards take them in
+// parallel.  The sharding is by block index, so it is correct under any placement; under the observed
+// round-robin dealing a shard is one XCD.  Then one lane polls the go word (bounded, Watchdog), ONE
+// agent-scope acquire, and the workgroup barrier releases every wave.  False (workgroup-uniform) when
+// the wait gave up: the workgroup then skips what is left of the launch.
+__device__ __forceinline__ bool grid_barrier_words(uint32_t* top, uint32_t* shards, uint32_t* go, uint32_t k,
+                                                   const Watchdog& wd) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores (and loads) are done
   __syncthreads();
   __shared__ uint32_t s_ok;
   if (threadIdx.x == 0) {
-    if (__hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == target - 1)
+    const uint32_t G = gridDim.x, sh = blockIdx.x & 7u;
+    const uint32_t ns = (G + 7u - sh) >> 3, nsh = G < 8u ? G : 8u;
+    if (__hip_atomic_fetch_add(shards + 32 * sh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k * ns - 1 &&
+        __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k * nsh - 1)
       __hip_atomic_store(go, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_ok = poll_bounded<4, 16, 32, 16, 32>(go, wd) ? 1u : 0u;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -384,10 +393,10 @@ __device__ __forceinline__ bool grid_barrier_words(uint32_t* counter, uint32_t* 
   return __builtin_amdgcn_readfirstlane(s_ok) != 0u;
 }
 // The in-place single launch's third barrier, between every final tile's loads and any store
-// (PassArgs: ipn_sync = the launch's sync words, ipn_go = the go word, ipn_strips = the arrival target)
+// (PassArgs: ipn_sync = the top counter, ipn_shards = the shard lines, ipn_go = the go word)
 template <class E>
 __device__ __forceinline__ bool ipn_grid_barrier(const PassArgs<E>& A) {
-  return grid_barrier_words(A.ipn_sync, A.ipn_go, A.ipn_strips, A.wd);
+  return grid_barrier_words(A.ipn_sync, A.ipn_shards, A.ipn_go, 3u, A.wd);
 }
 
 // LDS of one pass tile (words), and whether the pass stages its w_R^e table in LDS: E::LDS_TW
@@ -1009,7 +1018,7 @@ void k_fused3(const FusedKArgs<E> K) {
 // re-zeroes the words for the next launch.
 // False (workgroup-uniform) when the wait gave up (Watchdog): the workgroup then skips the passes left.
 __device__ __forceinline__ bool fused_grid_barrier(const FusedArgs& F, uint32_t k) {
-  return grid_barrier_words(F.sync, F.sync + F.rbase + 32 * (k - 1), k * gridDim.x, F.wd);
+  return grid_barrier_words(F.sync, F.shards, F.sync + F.rbase + 32 * (k - 1), k, F.wd);
 }
 
 template <class E, int R1, int R2, int R3>
@@ -1049,6 +1058,7 @@ void k_fused3b(const FusedKArgs<E> K) {
     if (F.wd.abort) __hip_atomic_store(F.wd.abort, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(F.sync + F.rbase, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(F.sync + F.rbase + 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t sh = 0; sh < 8; ++sh) __hip_atomic_store(F.shards + 32 * sh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1095,6 +1105,7 @@ void k_fused3bi(const FusedKArgs<E> K) {
     if (F.wd.abort) __hip_atomic_store(F.wd.abort, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (uint32_t k = 0; k < 3; ++k)
       __hip_atomic_store(F.sync + F.rbase + 32 * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t sh = 0; sh < 8; ++sh) __hip_atomic_store(F.shards + 32 * sh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

@@ -1174,7 +1174,7 @@ struct PlanImpl final : PlanBase {
           B.flags &= ~2u;
           B.ipn_sync = F.sync;
           B.ipn_go = F.sync + F.rbase + 64;  // the third barrier's go word
-          B.ipn_strips = 3 * F.nwg;          // its arrival target (the counter is cumulative)
+          B.ipn_shards = F.shards;           // its arrival shards (cumulative, like the top counter)
           B.wd = F.wd;
           e = launch_fused3<E>((int)r[0], (int)r[1], (int)r[2], out, nullptr, out, PA[0], PA[1], B, F, st);
           mark(st);
@@ -1277,13 +1277,15 @@ struct PlanImpl final : PlanBase {
     if (const char* v = getenv("NTT_FUSED_DBG")) F.dbg = (uint32_t)atoi(v);
     F.rbase = (4 + F.n12 + F.n23 + 31) & ~31u;
     const size_t words = F.rbase + 32 * (F.n12 + F.n23);  // then the abort word on a line of its own
-    if (hipMalloc(&d_sync, (words + 32) * 4) != hipSuccess) {
+    // then the abort word and the 8 barrier shards, each on a line of its own
+    if (hipMalloc(&d_sync, (words + 32 * 9) * 4) != hipSuccess) {
       d_sync = nullptr;
       return false;
     }
-    if (hipMemset(d_sync, 0, (words + 32) * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return false;
+    if (hipMemset(d_sync, 0, (words + 32 * 9) * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return false;
     F.sync = d_sync;
     F.wd.abort = d_sync + words;
+    F.shards = d_sync + words + 32;
     fargs = F;
     return true;
     }
@@ -1292,7 +1294,7 @@ struct PlanImpl final : PlanBase {
 
   // ---- the in-place single launch (NTT_PLAN_SINGLE_LAUNCH on an NTT_PLAN_IN_PLACE plan, k_fused3bi):
   // 3-pass palindromic FAST 256-bit schedules whose tiles all fit the device at once (2^18 .. 2^20)
-  uint32_t* d_sync_ip = nullptr;  // [0] arrivals, [1] exits; go words at 32, 64, 96; abort at 128
+  uint32_t* d_sync_ip = nullptr;  // [0] top arrivals, [1] exits; go words at 32, 64, 96; abort at 128; shards at 160
   FusedArgs fargs_ip{};
   bool fused_ip_built = false, fused_ip_ok = false;
   bool fused_ip_ready(const PassArgs<E>* PA) {
@@ -1318,13 +1320,15 @@ struct PlanImpl final : PlanBase {
       if (const char* v = getenv("NTT_FUSED_VERBOSE"))
         fprintf(stderr, "libntt: in-place single launch, %u tiles per pass, %u workgroups (capacity %u)\n", tiles,
                 tiles, cap);
-      if (hipMalloc(&d_sync_ip, 160 * 4) != hipSuccess) {  // go words at 32, 64, 96; abort at 128
+      // go words at 32, 64, 96; abort at 128; barrier shards at 160 + 32 s
+      if (hipMalloc(&d_sync_ip, 416 * 4) != hipSuccess) {
         d_sync_ip = nullptr;
         return false;
       }
-      if (hipMemset(d_sync_ip, 0, 160 * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return false;
+      if (hipMemset(d_sync_ip, 0, 416 * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return false;
       F.sync = d_sync_ip;
       F.wd.abort = d_sync_ip + 128;
+      F.shards = d_sync_ip + 160;
       fargs_ip = F;
       return true;
     }

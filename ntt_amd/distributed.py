@@ -381,6 +381,41 @@ class DistNTT:
         self._x_windows: Optional[list] = None
         self._x_open: Optional[list] = None
 
+    def tune_pieces(self, x: torch.Tensor, candidates=None, steps: int = 8, warmup: int = 3) -> dict:
+        """Plan-time measurement of the exchange schedule (FFTW_MEASURE-style), collective over the
+        group: every rank times forward(x) with each candidate (row pieces, column pieces) -- by
+        default 1 x 1 and the auto_pieces rule -- the slowest rank's time counts, and the fastest
+        candidate becomes this plan's schedule.  Whether pieces pay depends on the link rate against
+        the local transforms, which only the node at hand can say.  x is overwritten."""
+        import time as _t
+        L = self.layout
+        if candidates is None:
+            auto = (self.auto_pieces(L.local_n),
+                    self.auto_pieces(L.local_n, cap=4, min_elems=self.MIN_COL_PIECE_ELEMS))
+            candidates = [(1, 1)] + ([auto] if auto != (1, 1) else [])
+        dev = x.device if not self.host_exchange else torch.device("cpu")
+        results = {}
+        best = None
+        for p, q in candidates:
+            fs = FourStep(L, self.engine, self, pieces=p, col_pieces=q)
+            self.fs = fs
+            for _ in range(warmup):
+                fs.forward(x)
+            torch.cuda.synchronize()
+            self.dist.barrier(group=self.group)
+            t0 = _t.perf_counter()
+            for _ in range(steps):
+                fs.forward(x)
+            torch.cuda.synchronize()
+            dt = torch.tensor([(_t.perf_counter() - t0) / steps], dtype=torch.float64, device=dev)
+            self.dist.all_reduce(dt, op=self.dist.ReduceOp.MAX, group=self.group)
+            key = f"{len(fs.pieces)}x{fs.cp}"
+            results[key] = float(dt.item()) * 1e3
+            if best is None or results[key] < best[0]:
+                best = (results[key], fs, key)
+        self.fs = best[1]
+        return {"chosen": best[2], "ms_per_transform": results, "steps": steps, "warmup": warmup}
+
     # RCCL moves < 2 GiB per peer per collective (a 2 GiB chunk arrived half copied,
     # tests/test_gpu_fullsize.py): larger per-peer runs go as several all-to-alls.
     MAX_PEER_BYTES = 1 << 30
