@@ -211,6 +211,32 @@ class FourStep:
         return self._inverse(a, b, out)
 
 
+def tune_four_step(layout: Layout, engine, exchange, dist, group, x, candidates, steps: int, warmup: int,
+                   device, sync: Callable[[], None]):
+    """Time forward(x) under each candidate (row pieces, column pieces) on every rank of `group`, in
+    the same order on every rank; a candidate's time is the slowest rank's (all_reduce MAX), so every
+    rank picks the same schedule.  Returns (the fastest FourStep, {"chosen", "ms_per_transform", ...})."""
+    import time as _t
+    results, best = {}, None
+    for p, q in candidates:
+        fs = FourStep(layout, engine, exchange, pieces=p, col_pieces=q)
+        for _ in range(warmup):
+            fs.forward(x)
+        sync()
+        dist.barrier(group=group)
+        t0 = _t.perf_counter()
+        for _ in range(steps):
+            fs.forward(x)
+        sync()
+        dt = torch.tensor([(_t.perf_counter() - t0) / max(1, steps)], dtype=torch.float64, device=device)
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX, group=group)
+        key = f"{len(fs.pieces)}x{fs.cp}"
+        results[key] = float(dt.item()) * 1e3
+        if best is None or results[key] < best[0]:
+            best = (results[key], fs, key)
+    return best[1], {"chosen": best[2], "ms_per_transform": results, "steps": steps, "warmup": warmup}
+
+
 class _WholeExchange:
     """Adapter for a plain ``exchange(send, recv)`` callable: whole-block all-to-all, one piece."""
 
@@ -382,39 +408,19 @@ class DistNTT:
         self._x_open: Optional[list] = None
 
     def tune_pieces(self, x: torch.Tensor, candidates=None, steps: int = 8, warmup: int = 3) -> dict:
-        """Plan-time measurement of the exchange schedule (FFTW_MEASURE-style), collective over the
-        group: every rank times forward(x) with each candidate (row pieces, column pieces) -- by
-        default 1 x 1 and the auto_pieces rule -- the slowest rank's time counts, and the fastest
-        candidate becomes this plan's schedule.  Whether pieces pay depends on the link rate against
-        the local transforms, which only the node at hand can say.  x is overwritten."""
-        import time as _t
+        """Plan-time measurement of the exchange schedule (FFTW_MEASURE-style; tune_four_step): every
+        rank times forward(x) with 1 x 1 and the auto_pieces rule, and the fastest becomes this plan's
+        schedule.  Whether pieces pay depends on the link rate against the local transforms, which only
+        the node at hand can say.  Collective over the group; x is overwritten."""
         L = self.layout
         if candidates is None:
             auto = (self.auto_pieces(L.local_n),
                     self.auto_pieces(L.local_n, cap=4, min_elems=self.MIN_COL_PIECE_ELEMS))
             candidates = [(1, 1)] + ([auto] if auto != (1, 1) else [])
-        dev = x.device if not self.host_exchange else torch.device("cpu")
-        results = {}
-        best = None
-        for p, q in candidates:
-            fs = FourStep(L, self.engine, self, pieces=p, col_pieces=q)
-            self.fs = fs
-            for _ in range(warmup):
-                fs.forward(x)
-            torch.cuda.synchronize()
-            self.dist.barrier(group=self.group)
-            t0 = _t.perf_counter()
-            for _ in range(steps):
-                fs.forward(x)
-            torch.cuda.synchronize()
-            dt = torch.tensor([(_t.perf_counter() - t0) / steps], dtype=torch.float64, device=dev)
-            self.dist.all_reduce(dt, op=self.dist.ReduceOp.MAX, group=self.group)
-            key = f"{len(fs.pieces)}x{fs.cp}"
-            results[key] = float(dt.item()) * 1e3
-            if best is None or results[key] < best[0]:
-                best = (results[key], fs, key)
-        self.fs = best[1]
-        return {"chosen": best[2], "ms_per_transform": results, "steps": steps, "warmup": warmup}
+        dev = torch.device("cpu") if self.host_exchange else x.device
+        self.fs, res = tune_four_step(L, self.engine, self, self.dist, self.group, x, candidates, steps, warmup,
+                                      dev, torch.cuda.synchronize)
+        return res
 
     # RCCL moves < 2 GiB per peer per collective (a 2 GiB chunk arrived half copied,
     # tests/test_gpu_fullsize.py): larger per-peer runs go as several all-to-alls.

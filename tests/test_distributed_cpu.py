@@ -204,3 +204,55 @@ def test_piece_ranges_and_auto_pieces():
     # 2^24 over 2 GPUs (2^23 per rank): 2 row pieces, 4 column pieces; over 8 (2^21): none
     assert DistNTT.auto_pieces(1 << 23, cap=4, min_elems=DistNTT.MIN_COL_PIECE_ELEMS) == 4
     assert DistNTT.auto_pieces(1 << 21, cap=4, min_elems=DistNTT.MIN_COL_PIECE_ELEMS) == 1
+
+
+def _tune_worker(rank, world, port, field_id, log_n, L, q):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from ntt_amd.distributed import Layout, tune_four_step
+    from tests.dist_helpers import CpuOracleEngine, GlooPieceExchange, row_shares
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n = 1 << log_n
+        x = R.random_vector(field_id, n, seed=78)
+        share = row_shares(x, Layout, log_n, world, L)[rank]
+        eng = CpuOracleEngine(field_id, log_n, L, world, rank)
+        lay = Layout(log_n, world, rank)
+        scratch = share.clone()
+        fs, res = tune_four_step(lay, eng, GlooPieceExchange(lay), dist, None, scratch, [(1, 1), (2, 2), (4, 1)],
+                                 steps=1, warmup=0, device=torch.device("cpu"), sync=lambda: None)
+        fs.forward(share)  # the chosen schedule computes the same transform
+        q.put((rank, share.numpy().tobytes(), res["chosen"], sorted(res["ms_per_transform"])))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tune_four_step_picks_one_schedule_on_every_rank():
+    """DistNTT.tune_pieces' collective core (tune_four_step): every rank times the candidates in the
+    same order, takes the slowest rank's time, and so picks the SAME schedule; that schedule's
+    forward equals the definition."""
+    from ntt_amd.distributed import Layout
+    from tests.dist_helpers import gather_cols
+    world, field_id, log_n, L = 4, 1, 8, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tune_worker, args=(r, world, port, field_id, log_n, L, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rank, fwd, chosen, keys = q.get(timeout=240)
+        res[rank] = (fwd, chosen, keys)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import numpy as np
+    assert len({res[r][1] for r in range(world)}) == 1, res
+    assert res[0][2] == ["1x1", "2x2", "4x1"]
+    shares = [torch.from_numpy(np.frombuffer(res[r][0], dtype=np.int64).copy().reshape(-1, L)) for r in range(world)]
+    X = gather_cols(shares, Layout, log_n, world, L)
+    p_, g_ = R.FIELDS[field_id]
+    assert X == R.ntt_dit(R.random_vector(field_id, 1 << log_n, seed=78), p_, g_)
