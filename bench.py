@@ -423,8 +423,10 @@ def main():
         data = eng.empty()
         tuned = None
         if world > 1 and args.pieces is None and args.col_pieces is None:
-            # the exchange schedule is chosen by measurement on this node (DistNTT.tune_pieces)
-            tuned = eng.tune_pieces(data if not args.inverse else eng.empty())
+            # the exchange schedule is chosen by measurement on this node (DistNTT.tune_pieces) on a
+            # canonical vector, then the data is filled again
+            eng.fill(data, "random", seed=2)
+            tuned = eng.tune_pieces(data)
         eng.fill(data, "random", seed=2)
         step = (lambda: eng.inverse(data)) if args.inverse else (lambda: eng.forward(data))
         plan_for_prof = eng
