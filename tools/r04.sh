@@ -15,7 +15,9 @@ step() {  # name seconds cmd...
   if [ $rc -ne 0 ]; then tail -40 $O/$name.log >&2; exit $rc; fi
 }
 PYT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
-for s in "$@"; do
+ARGS="$@"
+[ "$ARGS" = final ] && ARGS="tests smoke bench prof pmc configs fs1 reh2"
+for s in $ARGS; do
   case $s in
     new) step pytest_new 400 $PYT tests/test_gpu_mplan_copy.py tests/test_gpu_watchdog.py ;;
     sl) step pytest_sl 600 $PYT tests/test_gpu_single_launch.py tests/test_gpu_inplace.py tests/test_gpu_watchdog.py ;;
