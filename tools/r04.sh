@@ -54,6 +54,7 @@ for s in $ARGS; do
         cat $O/c2_ab_m0_$rep.log | grep '^{' | sed "s/^/mode0 /" >> $O/c2_ab.txt
       done
       step c2_prof 300 rocprofv3 --kernel-trace --stats -d $O/c2prof -o run --output-format csv -- python3 tools/exp_launches.py $C --warmup 20 --steps 100 ;;
+    abmmc) step ab_mmc 600 tools/exp_variants.sh mmc ;;
     configs) step configs 600 python -u tools/bench_configs.py --out $O/configs.jsonl ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
   esac
