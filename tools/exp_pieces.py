@@ -24,15 +24,22 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default="")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--cfg", action="append", default=[], help="world,log_n,row_pieces,col_pieces (repeatable)")
+    ap.add_argument("--forward-only", action="store_true")
+    ap.add_argument("--extra-streams", type=int, default=0,
+                    help="create this many torch streams first (moves the side stream to another hardware queue)")
     a = ap.parse_args()
+    cfgs = [tuple(int(v) for v in c.split(",")) for c in a.cfg] or CFGS
     import torch
     from ntt_amd.distributed import VirtualRanks
+    keep = [torch.cuda.Stream() for _ in range(a.extra_streams)]
     rows = []
-    for world, lg, rp, cp in CFGS:
+    for world, lg, rp, cp in cfgs:
         vr = VirtualRanks(1, lg, 4, world, pieces=rp, col_pieces=cp)
         xs = vr.fill(vr.empty(), "random", seed=4)
         res = {"world": world, "log_n": lg, "row_pieces": vr.fs.rp, "col_pieces": vr.fs.cp}
-        for name, fn in (("forward_ms", vr.forward), ("inverse_ms", vr.inverse)):
+        runs = (("forward_ms", vr.forward),) if a.forward_only else (("forward_ms", vr.forward), ("inverse_ms", vr.inverse))
+        for name, fn in runs:
             for _ in range(3):
                 fn(xs)
             torch.cuda.synchronize()

@@ -55,6 +55,18 @@ for s in $ARGS; do
       done
       step c2_prof 300 rocprofv3 --kernel-trace --stats -d $O/c2prof -o run --output-format csv -- python3 tools/exp_launches.py $C --warmup 20 --steps 100 ;;
     abmmc) step ab_mmc 600 tools/exp_variants.sh mmc ;;
+    ptrace)  # C4 over 8 virtual ranks: kernel + copy traces of the piece schedules
+      for c in 1,1 4,4 4,1 1,4; do
+        t=$(echo $c | tr , x)
+        step ptrace_$t 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d $O/ptrace_$t -o run --output-format csv -- python3 tools/exp_pieces.py --cfg 8,28,$c --reps 3 --forward-only
+      done ;;
+    ptrace_seq)  # the same configs in ONE process, in bench_configs.py's order (1x1, 4x1, 4x4)
+      step ptrace_seq 400 rocprofv3 --kernel-trace --stats -d $O/ptrace_seq -o run --output-format csv -- python3 tools/exp_pieces.py --cfg 8,28,1,1 --cfg 8,28,4,1 --cfg 8,28,4,4 --reps 3 --forward-only ;;
+    ptrace_q)  # 4 x 4 with 0..3 extra streams created first: which hardware queue the side stream gets
+      for k in 0 1 2 3; do
+        step ptrace_q$k 300 rocprofv3 --kernel-trace -d $O/ptrace_q$k -o run --output-format csv -- python3 tools/exp_pieces.py --cfg 8,28,4,4 --reps 3 --forward-only --extra-streams $k
+      done ;;
+    ctrace) step configs_trace 600 rocprofv3 --kernel-trace -d $O/ctrace -o run --output-format csv -- python3 tools/bench_configs.py --out $O/configs_traced.jsonl ;;
     configs) step configs 600 python -u tools/bench_configs.py --out $O/configs.jsonl ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
   esac
