@@ -543,9 +543,11 @@ class VirtualRanks:
     """
 
     def __init__(self, field_id: int, log_n: int, limbs64: int, world: int, device: int = 0, pieces: int = 1,
-                 col_pieces: Optional[int] = None):
-        """col_pieces: column pieces (None: as many as row pieces)."""
+                 col_pieces: Optional[int] = None, batched: bool = False):
+        """col_pieces: column pieces (None: as many as row pieces).  batched: every exchange unit's
+        copies as one multi-tensor copy (torch._foreach_copy_) instead of one device copy each."""
         self.world = world
+        self.batched = batched
         self.engines = [RankPlan(field_id, log_n, limbs64, world, g, device) for g in range(world)]
         self.layout0 = self.engines[0].layout
         self.layouts = [e.layout for e in self.engines]
@@ -565,10 +567,13 @@ class VirtualRanks:
         with torch.cuda.stream(self.side):
             sv = [run_views(t, G, peer_stride, runs) for t in sends]
             rv = [run_views(t, G, peer_stride, runs) for t in recvs]
-            for dst in range(G):
-                for src in range(G):
-                    for u in range(len(runs)):
-                        rv[dst][src][u].copy_(sv[src][dst][u])
+            pairs = [(rv[dst][src][u], sv[src][dst][u]) for dst in range(G) for src in range(G)
+                     for u in range(len(runs))]
+            if self.batched:  # one multi-tensor copy launch instead of G*G*runs blit kernels
+                torch._foreach_copy_([d for d, _ in pairs], [s for _, s in pairs])
+            else:
+                for d, s in pairs:
+                    d.copy_(s)
             done = torch.cuda.Event()
             done.record()
         for t in list(sends) + list(recvs):  # the side stream uses them: keep the caching allocator honest

@@ -29,6 +29,7 @@ def _eq_at(t, src, idx, chunk=1 << 22):
     return all(torch.equal(t[i:i + chunk], src[idx[i:i + chunk]]) for i in range(0, idx.numel(), chunk))
 
 
+@pytest.mark.parametrize("batched", [False, True])
 @pytest.mark.parametrize("world,log_n,field_id,L,pieces,col_pieces",
                          [(1, 12, 1, 4, 1, 1), (2, 12, 1, 4, 1, 1), (4, 16, 1, 4, 1, 1), (8, 20, 1, 4, 1, 1),
                           (8, 16, 2, 6, 1, 1), (2, 14, 0, 1, 1, 1), (2, 12, 1, 4, 4, 1), (8, 20, 1, 4, 4, 1),
@@ -37,8 +38,8 @@ def _eq_at(t, src, idx, chunk=1 << 22):
                           (2, 12, 1, 4, 1, 4), (2, 12, 1, 4, 4, 4), (8, 20, 1, 4, 4, 4), (4, 16, 1, 4, 2, 8),
                           (2, 14, 0, 1, 2, 2), (8, 16, 2, 6, 2, 2), (4, 22, 1, 4, 4, 4), (2, 24, 1, 4, 2, 2),
                           (1, 26, 1, 4, 4, 8)])
-def test_virtual_ranks_match_single_gpu(world, log_n, field_id, L, pieces, col_pieces):
-    """pieces / col_pieces > 1: the pipelined schedule (the exchange units copied on a side stream
+def test_virtual_ranks_match_single_gpu(world, log_n, field_id, L, pieces, col_pieces, batched):
+    """batched: each exchange unit's copies as one multi-tensor copy.  pieces / col_pieces > 1: the pipelined schedule (the exchange units copied on a side stream
     while the row transforms before them and the column transforms after them run) -- same column
     layout, same round trip.  2^22 / 2^24 / 2^26: the rank plans' unbalanced split (n2 = 2^10, one
     workgroup tile per row transform); 2^26 at world 1 has 2^16 rows per rank, launched in chunks of
@@ -50,7 +51,7 @@ def test_virtual_ranks_match_single_gpu(world, log_n, field_id, L, pieces, col_p
     ref.fill(x, "random", seed=42)
     x0 = x.clone()
     ref.forward(x)
-    vr = VirtualRanks(field_id, log_n, L, world, pieces=pieces, col_pieces=col_pieces)
+    vr = VirtualRanks(field_id, log_n, L, world, pieces=pieces, col_pieces=col_pieces, batched=batched)
     xs = vr.fill(vr.empty(), "random", seed=42)
     for lay, t in zip(vr.layouts, xs):  # row-layout shares hold the right global elements
         assert _eq_at(t, x0, _index(lay, "row"))

@@ -69,12 +69,13 @@ def _single_gpu_product(fid, L, log_n, seed_a, seed_b):
                                                              (2, 0, 1, 14, False, 2), (2, 1, 4, 12, False, 2),
                                                              (2, 1, 4, 22, False, 4)])
 def test_virtual_ranks_polymul_matches_single_gpu(world, fid, L, log_n, square, pieces):
-    """pieces > 1: as many row and column pieces (VirtualRanks' default); the P field (no fused
+    """pieces > 1: as many row and column pieces (VirtualRanks' default), exchanged as one
+    multi-tensor copy per unit (batched); the P field (no fused
     product) and 2^12 over 2 (single-pass column transforms) take the gathered-product path of
     ntt_rplan_inverse_cols_piece."""
     from ntt_amd.distributed import VirtualRanks
     exp = _single_gpu_product(fid, L, log_n, 5, None if square else 6)
-    vr = VirtualRanks(fid, log_n, L, world, pieces=pieces)
+    vr = VirtualRanks(fid, log_n, L, world, pieces=pieces, batched=pieces > 1)
     As = vr.fill(vr.empty(), "random", seed=5)
     Bs = As if square else vr.fill(vr.empty(), "random", seed=6)
     Outs = vr.empty()
@@ -83,12 +84,14 @@ def test_virtual_ranks_polymul_matches_single_gpu(world, fid, L, log_n, square, 
         assert torch.equal(o, exp[_row_index(lay, o.device)]), (world, log_n, lay.rank)
 
 
-def test_c5_polymul_2pow24_eight_virtual_ranks():
-    """BASELINE config 5's size and GPU count, on one GPU: bit-exact vs the single-GPU product."""
+@pytest.mark.parametrize("batched", [False, True])
+def test_c5_polymul_2pow24_eight_virtual_ranks(batched):
+    """BASELINE config 5's size and GPU count, on one GPU: bit-exact vs the single-GPU product.
+    batched: each exchange unit's copies as one multi-tensor copy."""
     from ntt_amd.distributed import VirtualRanks
     fid, L, log_n, world = 1, 4, 24, 8
     exp = _single_gpu_product(fid, L, log_n, 5, 6)
-    vr = VirtualRanks(fid, log_n, L, world, pieces=4)  # the pipelined exchange, as timed in bench_configs
+    vr = VirtualRanks(fid, log_n, L, world, pieces=4, batched=batched)  # the pipelined exchange, as timed in bench_configs
     As = vr.fill(vr.empty(), "random", seed=5)
     Bs = vr.fill(vr.empty(), "random", seed=6)
     vr.polymul(As, Bs, As)  # out aliases a

@@ -67,6 +67,15 @@ for s in $ARGS; do
         step ptrace_q$k 300 rocprofv3 --kernel-trace -d $O/ptrace_q$k -o run --output-format csv -- python3 tools/exp_pieces.py --cfg 8,28,4,4 --reps 3 --forward-only --extra-streams $k
       done ;;
     ctrace) step configs_trace 600 rocprofv3 --kernel-trace -d $O/ctrace -o run --output-format csv -- python3 tools/bench_configs.py --out $O/configs_traced.jsonl ;;
+    c5d) step c5dist_1 200 python3 -u tools/exp_c5dist.py --pieces 1 && step c5dist_4 200 python3 -u tools/exp_c5dist.py --pieces 4 ;;
+    c5b)  # the same with every exchange unit as one multi-tensor copy, and C4 forwards both ways
+      X="python3 -u tools/exp_c5dist.py --no-profile"
+      step c5b_1 200 $X --batched --pieces 1 && step c5b_4 200 $X --batched --pieces 4 &&
+      step c4_1 200 $X --log-n 28 --ops forward --steps 5 --pieces 1 &&
+      step c4_1b 200 $X --log-n 28 --ops forward --steps 5 --pieces 1 --batched &&
+      step c4_4 200 $X --log-n 28 --ops forward --steps 5 --pieces 4 &&
+      step c4_4b 200 $X --log-n 28 --ops forward --steps 5 --pieces 4 --batched ;;
+    c5dt) step c5dist_trace 300 rocprofv3 --kernel-trace --stats -d $O/c5dt -o run --output-format csv -- python3 tools/exp_c5dist.py --pieces 1 --steps 10 ;;
     configs) step configs 600 python -u tools/bench_configs.py --out $O/configs.jsonl ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
   esac
