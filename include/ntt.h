@@ -108,8 +108,14 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
  * 2^20 as 4 launches, GZKP-NTT.cu:1509-1545): a 3-pass forward / inverse of a 4-limb BN254 / BLS12-381
  * plan (2^18 .. 2^24) runs as ONE persistent launch: two grid-wide barriers in a cooperative launch
  * (k_fused3b; the default) or the passes' tiles handed between workgroups through dependency
- * counters (k_fused3; environment NTT_FUSED_MODE=0), instead of kernel boundaries.  Same contract
+ * counters (k_fused3; environment NTT_FUSED_MODE=0), instead of kernel boundaries.  With
+ * NTT_PLAN_IN_PLACE too (2^18 .. 2^20): no scratch, three grid barriers (k_fused3bi).  Same contract
  * and results as the default schedule; batch 1; other plans and calls ignore the flag.
+ * The cooperative launch costs ~20 us per call (it guarantees that every workgroup is resident at
+ * once).  Environment NTT_FUSED_COOP=0 launches the grid-barrier forms as plain launches, after the
+ * plan has checked that the grid fits the device: 2^18 then ties three launches, 2^20 comes within
+ * ~4 %.  Only for a process that never runs two single-launch plans at once: two such kernels on
+ * different streams can each hold part of the device and wait for the other, until the watchdog.
  * ntt_plan_device_status reports a wait that gave up (a watchdog; never expected). */
 #define NTT_PLAN_SINGLE_LAUNCH 32u
 int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags);

@@ -1119,15 +1119,19 @@ hipError_t launch_fused3(int r1, int r2, int r3, const uint32_t* src, uint32_t* 
     const dim3 g(F.nwg), b((1 << E::TILE_LOG) / E::EPT);
     FusedKArgs<E> K{src, scratch, dst, A1, A2, A3, F};
     void* kargs[] = {&K};
-    static const bool coop = [] {  // NTT_FUSED_COOP=0: a plain launch of the grid-barrier form (A/B)
+    static const bool coop = [] {  // NTT_FUSED_COOP=0: a plain launch of the grid-barrier forms (A/B)
       const char* v = getenv("NTT_FUSED_COOP");
       return !(v && *v == '0');
     }();
     // mode 1: a cooperative launch (every workgroup resident, or the launch fails: never a hang)
     if (F.mode == 2) {  // in place: cooperative launch of exactly one workgroup per tile
 #define NTT_FUSED_IP_CASE(a, c, d)                                                                \
-  if (r1 == a && r2 == c && r3 == d)                                                              \
-    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_fused3bi<E, a, c, d>), g, b, kargs, 0, st);
+  if (r1 == a && r2 == c && r3 == d) {                                                            \
+    if (coop)                                                                                     \
+      return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_fused3bi<E, a, c, d>), g, b, kargs, 0, st); \
+    hipLaunchKernelGGL((k_fused3bi<E, a, c, d>), g, b, 0, st, K);                                 \
+    return hipGetLastError();                                                                     \
+  }
       NTT_FUSED_IP_CASE(6, 6, 6)
       NTT_FUSED_IP_CASE(6, 7, 6)
       NTT_FUSED_IP_CASE(7, 6, 7)

@@ -163,3 +163,36 @@ def test_in_place_single_launch_matches_default(fid, log_n):
         ip.inverse(a)
         assert torch.equal(a, x)
     assert ip.device_status() == 0
+
+
+_PLAIN_LAUNCH_CHECK = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+from ntt_amd.ntt import NTTPlan
+for log_n, ip in ((18, False), (20, False), (18, True), (20, True)):
+    ref = NTTPlan(1, log_n, 4)
+    one = NTTPlan(1, log_n, 4, single_launch=True, in_place=ip)
+    x = ref.fill(ref.empty(), "random", seed=7)
+    a, b = x.clone(), x.clone()
+    ref.forward(a)
+    for _ in range(3):  # repeated calls: the barrier words re-zero themselves
+        b.copy_(x)
+        one.forward(b)
+    assert torch.equal(a, b), (log_n, ip)
+    one.inverse(b)
+    assert torch.equal(b, x), (log_n, ip)
+    assert one.device_status() == 0
+print("plain-launch ok")
+"""
+
+
+def test_grid_barrier_forms_as_plain_launches():
+    """NTT_FUSED_COOP=0 (read once per process, so in a child process): the grid-barrier single
+    launches, default and in place, as plain launches give the default schedule's results."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, NTT_FUSED_COOP="0", NTT_FUSED_MODE="1")
+    r = subprocess.run([sys.executable, "-c", _PLAIN_LAUNCH_CHECK.format(root=root)], env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "plain-launch ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

@@ -54,6 +54,25 @@ for s in $ARGS; do
         cat $O/c2_ab_m0_$rep.log | grep '^{' | sed "s/^/mode0 /" >> $O/c2_ab.txt
       done
       step c2_prof 300 rocprofv3 --kernel-trace --stats -d $O/c2prof -o run --output-format csv -- python3 tools/exp_launches.py $C --warmup 20 --steps 100 ;;
+    coop)  # the grid-barrier single launches as a cooperative launch (default) and as a plain launch
+      L="--warmup 50 --steps 200"
+      C="--cfg f1_L4_n20 --cfg f1_L4_n20_sl --cfg f1_L4_n20_ip --cfg f1_L4_n20_ip_sl --cfg f1_L4_n18_sl --cfg f1_L4_n18_ip_sl"
+      for rep in 1 2; do
+        step coop1_$rep 200 python -u tools/exp_launches.py $C $L
+        grep '^{' $O/coop1_$rep.log | sed "s/^/coop /" >> $O/coop_ab.txt
+        step coop0_$rep 200 env NTT_FUSED_COOP=0 python -u tools/exp_launches.py $C $L
+        grep '^{' $O/coop0_$rep.log | sed "s/^/plain /" >> $O/coop_ab.txt
+      done
+      step coop0_sl 300 env NTT_FUSED_COOP=0 $PYT tests/test_gpu_single_launch.py ;;
+    coop2)  # 2^18 / 2^19: three launches against the plain-launch single launch, same box
+      L="--warmup 50 --steps 200"
+      C="--cfg f1_L4_n18 --cfg f1_L4_n18_sl --cfg f1_L4_n18_ip --cfg f1_L4_n18_ip_sl --cfg f1_L4_n19 --cfg f1_L4_n19_sl --cfg f1_L4_n19_ip --cfg f1_L4_n19_ip_sl --cfg f2_L4_n20 --cfg f2_L4_n20_sl"
+      for rep in 1 2; do
+        step coop2p_$rep 200 env NTT_FUSED_COOP=0 python -u tools/exp_launches.py $C $L
+        grep '^{' $O/coop2p_$rep.log | sed "s/^/plain /" >> $O/coop2_ab.txt
+        step coop2c_$rep 200 python -u tools/exp_launches.py $C $L
+        grep '^{' $O/coop2c_$rep.log | sed "s/^/coop /" >> $O/coop2_ab.txt
+      done ;;
     abmmc) step ab_mmc 600 tools/exp_variants.sh mmc ;;
     ptrace)  # C4 over 8 virtual ranks: kernel + copy traces of the piece schedules
       for c in 1,1 4,4 4,1 1,4; do
