@@ -215,11 +215,15 @@ int ntt_transpose_ex(ntt_plan* plan, const void* d_src, void* d_dst, unsigned lo
 /* Per-launch timing for benchmarks: when enabled, every transform records HIP events on its
  * stream between its kernel launches (a ring of 64 transforms, no host synchronisation);
  * ntt_plan_last_launch_ms returns per-launch durations (ms) averaged over the transforms recorded
- * since profiling was enabled (the last 64 at most), waiting for the most recent one. */
+ * since profiling was enabled (the last 64 at most), waiting for the most recent one; for the
+ * schedule the most recent call ran (single-vector or batched, see ntt_plan_info). */
 int ntt_plan_set_profiling(ntt_plan* plan, int enable);
 int ntt_plan_last_launch_ms(ntt_plan* plan, float* ms, unsigned max_launches, unsigned* nlaunches);
 
-/* Plan introspection: n, bytes per element, number of passes and their log2 radices. */
+/* Plan introspection: n, bytes per element, number of passes and their log2 radices (of a
+ * single-vector transform: a default or Montgomery-I/O 4 x 64-bit plan of exactly 2^20 runs those on
+ * 4096-element tiles in two passes, 10 + 10, and batched calls on 1024-element tiles, 7 + 7 + 6;
+ * environment NTT_WIDE_TILES=0 keeps every call on the latter). */
 int ntt_plan_info(const ntt_plan* plan, uint64_t* n, unsigned* elem_bytes, unsigned* npasses, unsigned radix_log[8]);
 int ntt_plan_destroy(ntt_plan* plan);
 const char* ntt_strerror(int status);

@@ -37,6 +37,7 @@ SOURCES += ["ntt_e256_stk.hip", "ntt_ep_stk.hip"]  # the bellperson-family rival
 SOURCES += ["ntt_e256_dit.hip", "ntt_ep_dit.hip"]  # the GZKP(B, G) rival schedule (NTT_PLAN_GZKP)
 SOURCES += [f"ntt_epi_{k}.hip" for k in ("col", "single", "fin", "misc")]  # P with 8-B scratch (NTT_PLAN_IN_PLACE)
 SOURCES += [f"ntt_e256wi_{k}.hip" for k in ("col", "single", "fin", "misc")]  # 48-B in place (NTT_PLAN_IN_PLACE)
+SOURCES += [f"ntt_e256t_{k}.hip" for k in ("col", "single", "fin", "misc")]  # 4096-element tiles (2^20 single transforms)
 SOURCES += ["ntt_plan.cpp", "ntt_rplan.cpp", "ntt_multi.cpp"]
 ARCH = os.environ.get("NTT_OFFLOAD_ARCH", "gfx950")
 

@@ -90,7 +90,7 @@ __device__ __forceinline__ void store_wt16(uint4* p, uint32_t a, uint32_t b, uin
 // Lazy bounds (units of p): the in-register DFTs take inputs < IN p (IN = 4: products < 3p,
 // reduced k = 0 outputs < 4p, HBM loads < p) and radix-2 stage s adds/subtracts with offset
 // IN 2^(s-1) p, so a Q-point DFT returns values < IN Q p <= 32p < B for every supported field.
-template <int L, int W32, int SCR_ = 0>
+template <int L, int W32, int SCR_ = 0, int TL_ = 0>
 struct Eng29 {
   static constexpr int W = L;                   // registers per element
   static constexpr int MEMW = W32;              // 32-bit words per element in HBM (canonical)
@@ -111,7 +111,9 @@ struct Eng29 {
   // sub-stages), 1024-element tiles (36 KiB LDS), 4 workgroups = 4 waves per SIMD.  384-bit class:
   // 8 elements per thread, 1024-element tiles, 2 waves per SIMD.
   static constexpr int EPT = (L <= 9) ? NTT_EPT_256 : 8;
-  static constexpr int TILE_LOG = (L <= 9) ? (EPT == 8 ? 11 : NTT_TILE_LOG_256) : 10;
+  // TL_ != 0 forces the tile: Eng256T's 4096-element tiles (one 1024-thread workgroup, 144 KiB of
+  // LDS, per CU), which run 2^20 in two passes (10 + 10) instead of three (7 + 7 + 6)
+  static constexpr int TILE_LOG = TL_ ? TL_ : ((L <= 9) ? (EPT == 8 ? 11 : NTT_TILE_LOG_256) : 10);
   static constexpr int WAVES_PER_EU = (L <= 9) ? (EPT == 4 ? NTT_WAVES_256 : 2) : 2;
   static constexpr bool LDS_SPLIT = false;
   static constexpr int MIN_COLS_LOG = 2;  // column passes own >= 4 adjacent columns: >= 128-B runs

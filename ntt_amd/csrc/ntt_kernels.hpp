@@ -27,6 +27,7 @@ using Eng256 = Eng29<9, 8>;    // 4 x 64-bit limbs in HBM
 using Eng384 = Eng29<14, 12>;  // 6 x 64-bit limbs in HBM, moduli up to 2^383
 using Eng256w = Eng29<9, 12>;  // 6 x 64-bit limbs in HBM, moduli < 2^255 (256-bit arithmetic)
 using Eng256wI = Eng29<9, 12, 12>;  // the same with 48-B intermediates: NTT_PLAN_IN_PLACE plans (C3 in place)
+using Eng256T = Eng29<9, 8, 0, 12>;  // 4 x 64-bit limbs, 4096-element tiles: single 2^20 transforms (C2)
 using EngP = Eng32<1, 2>;      // P469762049, `long long` in HBM
 using EngPI = Eng32<1, 2, 2>;  // the same with 8-B scratch elements: NTT_PLAN_IN_PLACE plans of P
 template <class E>

@@ -290,9 +290,9 @@ static bool schedule_palindrome(unsigned log_n, unsigned tile_log, unsigned rmax
 template <class E>
 struct EngHost;
 
-template <int L, int W32, int S>
-struct EngHost<Eng29<L, W32, S>> {
-  using E29 = Eng29<L, W32, S>;
+template <int L, int W32, int S, int T>
+struct EngHost<Eng29<L, W32, S, T>> {
+  using E29 = Eng29<L, W32, S, T>;
   static constexpr int NH = W32;
   static constexpr int TW = E29::TW;
   using EA = typename E29::Args;
@@ -1616,6 +1616,34 @@ static int make_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, const 
   return rc;
 }
 
+// BASELINE config 2 (2^20, 4 x 64-bit limbs): a single transform runs fastest on 4096-element tiles,
+// one 1024-thread workgroup per CU, in two passes (10 + 10) instead of three (7 + 7 + 6): 0.105
+// against 0.114 ms (BN254), 0.102 against 0.108 (BLS12-381), DESIGN §4.  Batched calls keep the
+// 1024-element tiles, which overlap the batch's transforms better (batch 4: 0.082 against 0.091 ms
+// per transform).  So a default 4-limb plan of 2^20 holds a second plan of 4096-element tiles for
+// one vector's transforms (forward, inverse, coset, polymul).  Environment NTT_WIDE_TILES=0: none.
+static bool wide_tiles_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("NTT_WIDE_TILES");
+    return !(v && *v == '0');
+  }();
+  return on;
+}
+
+static void make_wide_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, const uint64_t* g64,
+                           unsigned limbs64, unsigned log_n, int device, unsigned flags) {
+  if (limbs64 != 4 || log_n != 20 || (flags & ~NTT_PLAN_MONTGOMERY_IO) != 0 || !wide_tiles_enabled()) return;
+  uint32_t p32[12] = {0}, g32[12] = {0};
+  for (unsigned i = 0; i < 4; ++i) {
+    p32[2 * i] = (uint32_t)p64[i];
+    p32[2 * i + 1] = (uint32_t)(p64[i] >> 32);
+    g32[2 * i] = (uint32_t)g64[i];
+    g32[2 * i + 1] = (uint32_t)(g64[i] >> 32);
+  }
+  auto impl = std::make_unique<PlanImpl<Eng256T>>();
+  if (impl->init(p32, g32, log_n, device, flags) == NTT_OK) out = std::move(impl);  // else: the plan alone
+}
+
 static int set_err(int rc) {
   g_last_error = rc;
   return rc;
@@ -1625,6 +1653,13 @@ static int set_err(int rc) {
 
 struct ntt_plan {
   std::unique_ptr<PlanBase> impl;
+  std::unique_ptr<PlanBase> wide;  // one vector's transforms of a 2^20 4-limb plan (make_wide_plan)
+  PlanBase* last = nullptr;        // the plan that ran the latest transform (ntt_plan_last_launch_ms)
+  // The plan that transforms `batch` vectors, remembered for the profiling readers.
+  PlanBase& exec(unsigned batch) {
+    last = (wide && batch == 1) ? wide.get() : impl.get();
+    return *last;
+  }
 };
 
 extern "C" {
@@ -1636,7 +1671,9 @@ int ntt_plan_create_custom_ex(ntt_plan** out, const uint64_t* modulus, const uin
   std::unique_ptr<PlanBase> impl;
   int rc = make_plan(impl, modulus, generator, limbs64, log_n, device, flags);
   if (rc != NTT_OK) return set_err(rc);
-  *out = new ntt_plan{std::move(impl)};
+  std::unique_ptr<PlanBase> wide;
+  make_wide_plan(wide, modulus, generator, limbs64, log_n, device, flags);
+  *out = new ntt_plan{std::move(impl), std::move(wide)};
   return set_err(NTT_OK);
 }
 
@@ -1667,7 +1704,8 @@ int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned li
 extern "C++" template <class F>
 static int on_device(ntt_plan* plan, F&& f, bool check_watchdog = true) {
   if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
-  if (check_watchdog && plan->impl->tripped()) return set_err(NTT_ERR_DEVICE);
+  if (check_watchdog && (plan->impl->tripped() || (plan->wide && plan->wide->tripped())))
+    return set_err(NTT_ERR_DEVICE);
   int cur = 0;
   (void)hipGetDevice(&cur);
   if (cur != plan->impl->device) (void)hipSetDevice(plan->impl->device);
@@ -1679,20 +1717,21 @@ static int on_device(ntt_plan* plan, F&& f, bool check_watchdog = true) {
 extern "C++" inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
 
 int ntt_forward(ntt_plan* plan, void* d, void* s) {
-  return on_device(plan, [&](PlanBase& P) { return P.run(d, 1, false, S(s)); });
+  return on_device(plan, [&](PlanBase&) { return plan->exec(1).run(d, 1, false, S(s)); });
 }
 int ntt_inverse(ntt_plan* plan, void* d, void* s) {
-  return on_device(plan, [&](PlanBase& P) { return P.run(d, 1, true, S(s)); });
+  return on_device(plan, [&](PlanBase&) { return plan->exec(1).run(d, 1, true, S(s)); });
 }
 int ntt_forward_batch(ntt_plan* plan, void* d, unsigned b, void* s) {
-  return on_device(plan, [&](PlanBase& P) { return P.run(d, b, false, S(s)); });
+  return on_device(plan, [&](PlanBase&) { return plan->exec(b).run(d, b, false, S(s)); });
 }
 int ntt_inverse_batch(ntt_plan* plan, void* d, unsigned b, void* s) {
-  return on_device(plan, [&](PlanBase& P) { return P.run(d, b, true, S(s)); });
+  return on_device(plan, [&](PlanBase&) { return plan->exec(b).run(d, b, true, S(s)); });
 }
 
 static int run_coset(ntt_plan* plan, void* d, const uint64_t* shift, bool inv, void* s) {
-  return on_device(plan, [&](PlanBase& P) {
+  return on_device(plan, [&](PlanBase&) {
+    PlanBase& P = plan->exec(1);
     const unsigned limbs64 = P.elem_bytes >= 32 ? P.elem_bytes / 8 : 1;
     return P.coset(d, shift, limbs64, inv, S(s));
   });
@@ -1710,21 +1749,27 @@ int ntt_count_noncanonical(ntt_plan* plan, const void* d, uint64_t count, uint64
 
 int ntt_plan_device_status(ntt_plan* plan, unsigned* bad) {
   if (!bad) return set_err(NTT_ERR_ARG);
-  return on_device(plan, [&](PlanBase& P) { return P.device_status(bad); }, false);
+  return on_device(plan, [&](PlanBase& P) {
+    int rc = P.device_status(bad);
+    unsigned b2 = 0;
+    if (rc == NTT_OK && plan->wide && (rc = plan->wide->device_status(&b2)) == NTT_OK) *bad |= b2;
+    return rc;
+  }, false);
 }
 
 int ntt_plan_set_watchdog(ntt_plan* plan, unsigned spins) {
   if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
   plan->impl->wd_spins = spins;
+  if (plan->wide) plan->wide->wd_spins = spins;
   return set_err(NTT_OK);
 }
 
 int ntt_polymul(ntt_plan* plan, void* a, void* b, void* c, void* s) {
-  return on_device(plan, [&](PlanBase& P) { return P.polymul(a, b, c, S(s)); });
+  return on_device(plan, [&](PlanBase&) { return plan->exec(1).polymul(a, b, c, S(s)); });
 }
 
 int ntt_inverse_pointwise_batch(ntt_plan* plan, const void* a, const void* b, void* c, unsigned batch, void* s) {
-  return on_device(plan, [&](PlanBase& P) { return P.inverse_pointwise(a, b, c, batch, S(s)); });
+  return on_device(plan, [&](PlanBase&) { return plan->exec(batch).inverse_pointwise(a, b, c, batch, S(s)); });
 }
 
 int ntt_fill(ntt_plan* plan, void* d, int kind, uint64_t seed, void* s) {
@@ -1764,7 +1809,7 @@ int ntt_transpose_ex(ntt_plan* plan, const void* src, void* dst, unsigned log_ro
 
 int ntt_plan_info(const ntt_plan* plan, uint64_t* n, unsigned* elem_bytes, unsigned* npasses, unsigned radix_log[8]) {
   if (!plan || !plan->impl) return NTT_ERR_ARG;
-  const PlanBase& P = *plan->impl;
+  const PlanBase& P = plan->wide ? *plan->wide : *plan->impl;  // one vector's schedule
   if (n) *n = P.n;
   if (elem_bytes) *elem_bytes = P.elem_bytes;
   if (npasses) *npasses = P.npass;
@@ -1773,28 +1818,33 @@ int ntt_plan_info(const ntt_plan* plan, uint64_t* n, unsigned* elem_bytes, unsig
   return NTT_OK;
 }
 
-int ntt_plan_set_profiling(ntt_plan* plan, int enable) {
-  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
-  PlanBase& P = *plan->impl;
+static int set_profiling(PlanBase& P, int enable) {
   if (enable && !P.ev[0][0]) {
     int cur = 0;
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(P.device);
     for (auto& row : P.ev)
       for (auto& e : row)
-        if (hipEventCreate(&e) != hipSuccess) { (void)hipSetDevice(cur); return set_err(NTT_ERR_HIP); }
+        if (hipEventCreate(&e) != hipSuccess) { (void)hipSetDevice(cur); return NTT_ERR_HIP; }
     (void)hipSetDevice(cur);
   }
   P.profiling = enable != 0;
   P.nrec = 0;
-  return set_err(NTT_OK);
+  return NTT_OK;
+}
+
+int ntt_plan_set_profiling(ntt_plan* plan, int enable) {
+  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
+  int rc = set_profiling(*plan->impl, enable);
+  if (rc == NTT_OK && plan->wide) rc = set_profiling(*plan->wide, enable);
+  return set_err(rc);
 }
 
 // Average per-launch durations over the transforms recorded since profiling was enabled (at most
 // the last 64); waits for the most recent one.
 int ntt_plan_last_launch_ms(ntt_plan* plan, float* ms, unsigned max_launches, unsigned* nlaunches) {
   if (!plan || !plan->impl || !ms) return set_err(NTT_ERR_ARG);
-  PlanBase& P = *plan->impl;
+  PlanBase& P = plan->last ? *plan->last : *plan->impl;  // the plan that ran the latest transform
   const unsigned k = P.ev_used ? P.ev_used - 1 : 0;
   if (nlaunches) *nlaunches = k;
   if (k == 0 || P.nrec == 0) return set_err(NTT_OK);
@@ -1914,10 +1964,11 @@ static int blocking_forward(const std::shared_ptr<CachedPlan>& cp, void* d) {
   }
   if (rc == NTT_OK && (hipEventRecord(cp->done, nullptr) != hipSuccess || hipEventSynchronize(cp->done) != hipSuccess))
     rc = NTT_ERR_HIP;
-  PlanBase& P = *cp->plan->impl;
-  if (P.tripped()) {
-    P.clear_trip();
-    if (rc == NTT_OK) rc = NTT_ERR_DEVICE;
+  for (PlanBase* P : {cp->plan->impl.get(), cp->plan->wide.get()}) {
+    if (P && P->tripped()) {
+      P->clear_trip();
+      if (rc == NTT_OK) rc = NTT_ERR_DEVICE;
+    }
   }
   return set_err(rc);
 }

@@ -1,0 +1,132 @@
+"""BASELINE config 2 (2^20, 4 x 64-bit limbs) on 4096-element tiles: a default 4-limb plan of 2^20
+runs one vector's transforms (forward, inverse, coset, polymul, fused pointwise inverse) on a
+second plan of 4096-element tiles in two passes (10 + 10), and batched calls on the 1024-element
+tiles (7 + 7 + 6).  Checked bit for bit against the threaded C oracle (GZKP-NTT.cu:30-48, inverse
+GZKP-NTT.cu:1725-1732), against the batched path of the same plan, and against a child process
+with the second plan switched off (NTT_WIDE_TILES=0, read once per process) for every routed call."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ntt_ref as R
+from oracle import oracle_c as OC
+
+pytestmark = pytest.mark.gpu
+THREADS = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "8"))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _host(t):
+    return t.cpu().numpy().view(np.uint64).reshape(-1, 4)
+
+
+@pytest.mark.parametrize("fid", [1, 2])
+@pytest.mark.parametrize("kind", ["iota", "random"])
+def test_wide_tiles_vs_oracle(fid, kind):
+    from ntt_amd.ntt import NTTPlan
+    p, g = R.FIELDS[fid]
+    pl = NTTPlan(fid, 20, 4)
+    assert pl.passes == [10, 10]
+    t = pl.fill(pl.empty(), kind, seed=3)
+    x = _host(t).copy()
+    pl.set_profiling(True)
+    pl.forward(t)
+    assert len(pl.last_launch_ms()) == 2  # two passes
+    assert np.array_equal(_host(t), OC.ntt_mp_par(x, p, g, THREADS))
+    t.copy_(torch.from_numpy(x.view(np.int64)).to(t.device))
+    pl.inverse(t)
+    assert len(pl.last_launch_ms()) == 2
+    pl.set_profiling(False)
+    assert np.array_equal(_host(t), OC.ntt_mp_par(x, p, g, THREADS, inverse=True))
+    assert pl.device_status() == 0
+
+
+def test_batch_one_and_batched_paths_agree():
+    """Batch 1 runs on the 4096-element tiles (2 launches), batch 2 on the 1024-element tiles
+    (3 launches): same outputs, interleaved on one plan."""
+    from ntt_amd.ntt import NTTPlan
+    pl = NTTPlan(1, 20, 4)
+    n = pl.n
+    b = pl.empty(2)
+    bv = b.view(2, n, -1)
+    for i in range(2):
+        pl.fill(bv[i], "random", seed=11 + i)
+    x0, x1 = bv[0].clone(), bv[1].clone()
+    pl.set_profiling(True)
+    for _ in range(2):
+        pl.forward_batch(b, 2)
+        assert len(pl.last_launch_ms()) == 3
+        pl.forward(x0)
+        assert len(pl.last_launch_ms()) == 2
+        pl.forward(x1)
+        assert torch.equal(bv[0], x0) and torch.equal(bv[1], x1)
+        pl.inverse_batch(b, 2)
+        pl.inverse(x0)
+        pl.inverse(x1)
+        assert torch.equal(bv[0], x0) and torch.equal(bv[1], x1)
+    pl.set_profiling(False)
+
+
+_CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, {root!r})
+from ntt_amd.ntt import NTTPlan
+out = {{}}
+for fid in (1, 2):
+    for mont in (False, True):
+        pl = NTTPlan(fid, 20, 4, montgomery_io=mont)
+        a = pl.fill(pl.empty(), "random", seed=21 + fid)
+        b = pl.fill(pl.empty(), "random", seed=31 + fid)
+        c = pl.empty()
+        t = a.clone(); pl.forward(t); out[f"fwd{{fid}}{{int(mont)}}"] = t.cpu().numpy()
+        t = a.clone(); pl.inverse(t); out[f"inv{{fid}}{{int(mont)}}"] = t.cpu().numpy()
+        t = a.clone(); pl.forward_coset(t, 7); out[f"cf{{fid}}{{int(mont)}}"] = t.cpu().numpy()
+        t = a.clone(); pl.inverse_coset(t, 7); out[f"ci{{fid}}{{int(mont)}}"] = t.cpu().numpy()
+        pl.polymul(a.clone(), b.clone(), c); out[f"pm{{fid}}{{int(mont)}}"] = c.cpu().numpy()
+        pl.inverse_pointwise_batch(a, b, c, 1); out[f"ip{{fid}}{{int(mont)}}"] = c.cpu().numpy()
+        out[f"passes{{fid}}{{int(mont)}}"] = np.array(pl.passes)
+np.savez({path!r}, **out)
+print("child ok")
+"""
+
+
+def test_routed_calls_match_the_1024_tile_plan(tmp_path):
+    """forward, inverse, coset both ways, polymul and the fused pointwise inverse of a 2^20 plan
+    (BN254, BLS12-381; canonical and Montgomery I/O) against the same calls with NTT_WIDE_TILES=0."""
+    from ntt_amd.ntt import NTTPlan
+    path = str(tmp_path / "ref.npz")
+    env = dict(os.environ, NTT_WIDE_TILES="0")
+    r = subprocess.run([sys.executable, "-c", _CHILD.format(root=ROOT, path=path)], env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "child ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+    ref = np.load(path)
+    for fid in (1, 2):
+        for mont in (False, True):
+            k = f"{fid}{int(mont)}"
+            assert list(ref["passes" + k]) == [7, 7, 6]
+            pl = NTTPlan(fid, 20, 4, montgomery_io=mont)
+            assert pl.passes == [10, 10]
+            a = pl.fill(pl.empty(), "random", seed=21 + fid)
+            b = pl.fill(pl.empty(), "random", seed=31 + fid)
+            c = pl.empty()
+            t = a.clone(); pl.forward(t); assert np.array_equal(t.cpu().numpy(), ref["fwd" + k]), k
+            t = a.clone(); pl.inverse(t); assert np.array_equal(t.cpu().numpy(), ref["inv" + k]), k
+            t = a.clone(); pl.forward_coset(t, 7); assert np.array_equal(t.cpu().numpy(), ref["cf" + k]), k
+            t = a.clone(); pl.inverse_coset(t, 7); assert np.array_equal(t.cpu().numpy(), ref["ci" + k]), k
+            pl.polymul(a.clone(), b.clone(), c); assert np.array_equal(c.cpu().numpy(), ref["pm" + k]), k
+            pl.inverse_pointwise_batch(a, b, c, 1); assert np.array_equal(c.cpu().numpy(), ref["ip" + k]), k
+            assert pl.device_status() == 0
+
+
+def test_other_plans_keep_their_tiles():
+    """Only default (or Montgomery-I/O) 4-limb plans of exactly 2^20 take the second plan."""
+    from ntt_amd.ntt import NTTPlan
+    assert NTTPlan(1, 19, 4).passes == [7, 6, 6]
+    assert NTTPlan(1, 21, 4).passes == [7, 7, 7]
+    assert len(NTTPlan(1, 20, 4, in_place=True).passes) == 3
+    assert len(NTTPlan(1, 20, 4, single_launch=True).passes) == 3
+    assert len(NTTPlan(2, 20, 6).passes) == 3

@@ -73,6 +73,31 @@ for s in $ARGS; do
         step coop2c_$rep 200 python -u tools/exp_launches.py $C $L
         grep '^{' $O/coop2c_$rep.log | sed "s/^/coop /" >> $O/coop2_ab.txt
       done ;;
+    t12)  # 4096-element tiles (NTT_TILE_LOG_256=12, one 1024-thread workgroup per CU): 2^20 in two passes
+      L="--warmup 50 --steps 200"
+      C="--cfg f1_L4_n20 --cfg f2_L4_n20 --cfg f1_L4_n20_inv --cfg f1_L4_n18 --cfg f1_L4_n19 --cfg f1_L4_n21 --cfg f1_L4_n22 --cfg f1_L4_n24"
+      for rep in 1 2; do
+        step t12b_$rep 300 python -u tools/exp_launches.py $C $L
+        grep '^{' $O/t12b_$rep.log | sed "s/^/base /" >> $O/t12_ab.txt
+        step t12v_$rep 300 env NTT_LIB_PATH=ntt_amd/libntt_t12.so python -u tools/exp_launches.py $C $L
+        grep '^{' $O/t12v_$rep.log | sed "s/^/t12 /" >> $O/t12_ab.txt
+      done
+      step t12_parity 600 env NTT_LIB_PATH=ntt_amd/libntt_t12.so $PYT tests/test_gpu_parity.py ;;
+    t12batch)
+      for rep in 1 2; do
+        step t12batch_b$rep 300 python -u tools/exp_batch.py --log-n 20 --batches 1,2,4,8
+        step t12batch_v$rep 300 env NTT_LIB_PATH=ntt_amd/libntt_t12.so python -u tools/exp_batch.py --log-n 20 --batches 1,2,4,8
+      done ;;
+    wide)  # 2^20 4-limb plans: one vector's transforms on the 4096-element-tile plan (default) vs off
+      L="--warmup 50 --steps 200"
+      C="--cfg f1_L4_n20 --cfg f1_L4_n20_inv --cfg f2_L4_n20 --cfg f2_L4_n20_inv"
+      step wide_tests 600 $PYT tests/test_gpu_wide_tiles.py tests/test_gpu_single_launch.py tests/test_gpu_parity.py
+      for rep in 1 2; do
+        step wide1_$rep 200 python -u tools/exp_launches.py $C $L
+        grep '^{' $O/wide1_$rep.log | sed "s/^/wide /" >> $O/wide_ab.txt
+        step wide0_$rep 200 env NTT_WIDE_TILES=0 python -u tools/exp_launches.py $C $L
+        grep '^{' $O/wide0_$rep.log | sed "s/^/off /" >> $O/wide_ab.txt
+      done ;;
     abmmc) step ab_mmc 600 tools/exp_variants.sh mmc ;;
     ptrace)  # C4 over 8 virtual ranks: kernel + copy traces of the piece schedules
       for c in 1,1 4,4 4,1 1,4; do
