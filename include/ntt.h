@@ -118,6 +118,12 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
  * different streams can each hold part of the device and wait for the other, until the watchdog.
  * ntt_plan_device_status reports a wait that gave up (a watchdog; never expected). */
 #define NTT_PLAN_SINGLE_LAUNCH 32u
+/* Rival schedule, the reference's `naive` (GZKP-NTT.cu:59-95, big-num.cu:67-170): the bit reversal,
+ * then log2 n radix-2 DIT rounds of one launch each (a thread per butterfly, w from an n/2-entry power
+ * table, the reference's `roots`).  Forward single transforms of P469762049 and 4-limb plans; the
+ * plan's other calls run the default schedule.  Exclusive with the other rivals and with
+ * NTT_PLAN_IN_PLACE. */
+#define NTT_PLAN_NAIVE 64u
 int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags);
 /* Device-side status of a plan (blocking: synchronises the device, then reads and clears it).
  * *bad bit 0: an inter-workgroup wait gave up at its watchdog (NTT_PLAN_SINGLE_LAUNCH, or the fused

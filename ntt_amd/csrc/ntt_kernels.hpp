@@ -191,8 +191,16 @@ template <class E>
 hipError_t launch_build_tw_sh(uint32_t* out, size_t count, uint32_t log_r, uint32_t log_t, uint32_t log_m,
                               const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits, const typename E::Args& F,
                               const uint32_t* pinvB, hipStream_t st);
+// NTT_PLAN_NAIVE: the power table w_n^i R_e (i < count, E::TABW words per entry) and one radix-2
+// DIT round (stride 2^log_s) of the reference's `naive` rival over a bit-reversed vector
+template <class E>
+hipError_t launch_build_pow(uint32_t* out, size_t count, const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits,
+                            const typename E::Args& F, hipStream_t st);
+template <class E>
+hipError_t launch_naive_round(const uint32_t* src, uint32_t* dst, uint32_t log_n, uint32_t log_s, const uint32_t* pw,
+                              const typename E::Args& F, hipStream_t st);
 // dst[i] = src[digit reversal of i] over 2^log_n elements of E::MEMW words, digits of digits[q] bits
-// in pass order (the GZKP rival's `rearrange`; all 1 = the bit reversal)
+// in pass order (the GZKP rival's `rearrange`); nd = 0: the bit reversal (the naive rival's)
 template <class E>
 hipError_t launch_bitrev(const uint32_t* src, uint32_t* dst, uint32_t log_n, const uint32_t* digits, uint32_t nd,
                          hipStream_t st);

@@ -1275,6 +1275,59 @@ hipError_t launch_build_tw(uint32_t* out, size_t count, uint32_t log_r, uint32_t
   return hipGetLastError();
 }
 
+// NTT_PLAN_NAIVE (the reference's `naive` rival, GZKP-NTT.cu:59-71 / big-num.cu:67-104): the power
+// table entry i = w_n^i R_e mod p, i < count, canonical in the element format (E::TABW words) -- the
+// reference's `roots` table (GZKP-NTT.cu:81-83), built on the device from the two-level tables.
+template <class E>
+__global__ void k_build_pow(uint32_t* __restrict__ out, size_t count, const uint32_t* __restrict__ lo,
+                            const uint32_t* __restrict__ hi, uint32_t lo_bits, const typename E::Args F) {
+  NTT_GRID_STRIDE(i, count) {
+    typename E::Tw a, b;
+    E::tload(a, lo, i & ((size_t(1) << lo_bits) - 1));
+    E::tload(b, hi, i >> lo_bits);
+    E::mul(a.w, b, F);
+    E::template store<E::MUL_OUT, false, E::TABW>(out, i, a.w, F);
+  }
+}
+
+template <class E>
+hipError_t launch_build_pow(uint32_t* out, size_t count, const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits,
+                            const typename E::Args& F, hipStream_t st) {
+  hipLaunchKernelGGL((k_build_pow<E>), dim3(grid_1d(count)), dim3(256), 0, st, out, count, lo, hi, lo_bits, F);
+  return hipGetLastError();
+}
+
+// One radix-2 DIT round of the `naive` rival over a bit-reversed vector: butterfly id < n/2 pairs
+// pos = 2 (id - off) + off and pos + s (s = 2^log_s, off = id mod s) as (a + w b, a - w b) with
+// w = w_n^(off n / 2s) -- the reference kernel's indexing (GZKP-NTT.cu:59-71), one thread per
+// butterfly, canonical in and out (the product through the element-format power table: mulv).
+// HBM-bound by construction: every round reads and writes the whole vector.
+template <class E>
+__global__ void k_naive_round(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t log_n,
+                              uint32_t log_s, const uint32_t* __restrict__ pw, const typename E::Args F) {
+  const size_t half = size_t(1) << (log_n - 1), s = size_t(1) << log_s;
+  NTT_GRID_STRIDE(id, half) {
+    const size_t off = id & (s - 1), pos = ((id - off) << 1) + off;
+    uint32_t a[E::W], b[E::W], w[E::W];
+    E::load(a, src, pos);
+    E::load(b, src, pos + s);
+    E::template load<E::TABW>(w, pw, off << (log_n - 1 - log_s));
+    E::mulv(b, w, F);  // w R_e: the Montgomery product leaves w b, < 3p (Eng29) / < 2p (Eng32)
+    E::template bfly_l<E::IN>(a, b, F);
+    E::template store<2 * E::IN>(dst, pos, a, F);
+    E::template store<2 * E::IN>(dst, pos + s, b, F);
+  }
+}
+
+template <class E>
+hipError_t launch_naive_round(const uint32_t* src, uint32_t* dst, uint32_t log_n, uint32_t log_s, const uint32_t* pw,
+                              const typename E::Args& F, hipStream_t st) {
+  if (log_n == 0 || log_s >= log_n) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((k_naive_round<E>), dim3(grid_1d(size_t(1) << (log_n - 1))), dim3(256), 0, st, src, dst, log_n,
+                     log_s, pw, F);
+  return hipGetLastError();
+}
+
 // k_build_tw's table as Shoup pairs: entry (c, k) = (w, floor(w B / p)) with w = w_n^((c*k) << log_m)
 // canonical, in the engine's twiddle format (E::TW words).  t = lo_s * hi = w B mod p; w = t / B
 // (Montgomery product by 1); floor(w B / p) = (-(w B mod p)) p^-1 mod B (shoup_ws29).
@@ -1347,6 +1400,7 @@ __global__ void k_digitrev(const uint32_t* __restrict__ src, uint32_t* __restric
       j |= (rem & ((1ull << D.r[q]) - 1)) << top;
       rem >>= D.r[q];
     }
+    if (D.nd == 0) j = (size_t)(__brevll((unsigned long long)i) >> (64 - log_n));  // log_n 1-bit digits
     if constexpr (MEMW % 4 == 0) {
 #pragma unroll
       for (int q = 0; q < MEMW / 4; ++q)
@@ -1363,10 +1417,10 @@ hipError_t launch_bitrev(const uint32_t* src, uint32_t* dst, uint32_t log_n, con
                          hipStream_t st) {
   DigitRev D{};
   uint32_t sum = 0;
-  if (nd > 8) return hipErrorInvalidValue;
+  if (nd > 8 || log_n == 0 || log_n > 40) return hipErrorInvalidValue;
   D.nd = nd;
   for (uint32_t q = 0; q < nd; ++q) sum += (D.r[q] = digits[q]);
-  if (sum != log_n) return hipErrorInvalidValue;
+  if (nd > 0 && sum != log_n) return hipErrorInvalidValue;  // nd = 0: the bit reversal (digits unused)
   const size_t n = 1ull << log_n;
   hipLaunchKernelGGL((k_digitrev<E::MEMW>), dim3(grid_1d(n)), dim3(256), 0, st, src, dst, log_n,
                      D);
@@ -1922,6 +1976,10 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
   template hipError_t launch_scale_pow<E>(uint32_t*, uint32_t, uint32_t, const uint32_t*, const uint32_t*, uint32_t, \
                                           const typename E::Args&, hipStream_t);                                   \
   template hipError_t launch_count_noncanonical<E>(const uint32_t*, size_t, const ModWords<E::MEMW>&,              \
-                                                   unsigned long long*, hipStream_t);
+                                                   unsigned long long*, hipStream_t);                              \
+  template hipError_t launch_build_pow<E>(uint32_t*, size_t, const uint32_t*, const uint32_t*, uint32_t,           \
+                                          const typename E::Args&, hipStream_t);                                   \
+  template hipError_t launch_naive_round<E>(const uint32_t*, uint32_t*, uint32_t, uint32_t, const uint32_t*,       \
+                                            const typename E::Args&, hipStream_t);
 
 }  // namespace ntt

@@ -448,6 +448,8 @@ struct PlanImpl final : PlanBase {
   size_t off_hi_ipm = 0;                // inverse hi table scaled by n^-1 R_e (fused polymul, pass 1)
   uint32_t* d_full_pm = nullptr;        // inverse pass-1 outer twiddles x n^-1 R_e (fused polymul)
   uint32_t* d_stk_tab = nullptr;        // NTT_PLAN_STOCKHAM: per-pass input-twiddle tables
+  uint32_t* d_naive_pw = nullptr;       // NTT_PLAN_NAIVE: w_n^i R_e, i < n/2 (the reference's `roots`)
+  uint32_t* d_naive_buf = nullptr;      // NTT_PLAN_NAIVE: the bit-reversed copy the rounds work on
   size_t stk_off[8] = {};               // element offsets into d_stk_tab (pass >= 1)
   unsigned stk_ord[8] = {};             // Stockham pass i runs radix r[stk_ord[i]] (widest first)
   uint32_t* d_stk_buf[2] = {nullptr, nullptr};  // NTT_PLAN_STOCKHAM ping-pong buffers (E::MEMW words)
@@ -465,6 +467,8 @@ struct PlanImpl final : PlanBase {
     if (d_full_sh) (void)hipFree(d_full_sh);
     if (d_full_pm) (void)hipFree(d_full_pm);
     if (d_stk_tab) (void)hipFree(d_stk_tab);
+    if (d_naive_pw) (void)hipFree(d_naive_pw);
+    if (d_naive_buf) (void)hipFree(d_naive_buf);
     for (auto* p : d_stk_buf)
       if (p) (void)hipFree(p);
     if (d_bad) (void)hipFree(d_bad);
@@ -661,6 +665,7 @@ struct PlanImpl final : PlanBase {
     // NTT_PLAN_GZKP runs on the same per-pass tables: Stockham pass i's w_n^((k pi) << (log_n - lgp_i - r_i))
     // for k < 2^lgp_i is the GZKP DIT pass's w_N^(c d), N = 2^(lgp_i + r_i)
     if (rc == NTT_OK && (flags & (NTT_PLAN_STOCKHAM | NTT_PLAN_GZKP))) rc = build_stockham();
+    if (rc == NTT_OK && (flags & NTT_PLAN_NAIVE)) rc = build_naive();
     (void)hipSetDevice(cur);
     return rc;
   }
@@ -744,6 +749,35 @@ struct PlanImpl final : PlanBase {
       }
       return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
     }
+  }
+
+  // NTT_PLAN_NAIVE (rival schedule, the reference's `naive`, GZKP-NTT.cu:59-95 / big-num.cu:67-170):
+  // the bit reversal (`rearrange`), then log2 n radix-2 DIT rounds of one launch each, every round
+  // a full read and write of the vector (HBM-bound; the measure of what the pass kernels' fusion
+  // buys).  The reference's n-entry `roots` table is the n/2 entries its rounds read.
+  int build_naive() {
+    if constexpr (!HasStockham<E>::value) {
+      return NTT_ERR_ARG;  // the rival schedules: P and 4 x 64-bit plans
+    } else {
+      if (log_n < 1 || log_n > 32) return NTT_ERR_ARG;
+      const size_t half = n / 2;
+      if (hipMalloc(&d_naive_pw, half * TABW * 4) != hipSuccess) return NTT_ERR_HIP;
+      if (hipMalloc(&d_naive_buf, (size_t)n * MEMW * 4) != hipSuccess) return NTT_ERR_HIP;
+      if (launch_build_pow<E>(d_naive_pw, half, d_tab + off_los_f, d_tab + off_hi_f, lo_bits, Ff, nullptr) !=
+          hipSuccess)
+        return NTT_ERR_HIP;
+      return hipDeviceSynchronize() == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+    }
+  }
+
+  int run_naive(const uint32_t* in, uint32_t* out, hipStream_t st) {
+    begin(st);
+    hipError_t e = launch_bitrev<E>(in, d_naive_buf, log_n, nullptr, 0, st);  // radix-2 rounds: the bit reversal
+    mark(st);
+    for (unsigned s = 0; s < log_n && e == hipSuccess; ++s)
+      e = launch_naive_round<E>(d_naive_buf, s + 1 == log_n ? out : d_naive_buf, log_n, s, d_naive_pw, Ff, st);
+    mark(st);  // last_launch_ms: [bit reversal, all rounds]
+    return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
   }
 
   int run_stockham(const uint32_t* in, uint32_t* out, hipStream_t st) {
@@ -1035,6 +1069,8 @@ struct PlanImpl final : PlanBase {
       return run_stockham(static_cast<uint32_t*>(d), static_cast<uint32_t*>(d), st);
     if ((flags & NTT_PLAN_GZKP) && !inverse && batch == 1 && d_stk_tab)
       return run_gzkp(static_cast<uint32_t*>(d), static_cast<uint32_t*>(d), st);
+    if ((flags & NTT_PLAN_NAIVE) && !inverse && batch == 1 && d_naive_pw)
+      return run_naive(static_cast<uint32_t*>(d), static_cast<uint32_t*>(d), st);
     return run_io(static_cast<uint32_t*>(d), nullptr, static_cast<uint32_t*>(d), batch, inverse, st);
   }
 
@@ -1563,8 +1599,9 @@ static int make_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, const 
                      unsigned log_n, int device, unsigned flags) {
   if (log_n > 40) return NTT_ERR_ARG;
   if (limbs64 != 1 && limbs64 != 4 && limbs64 != 6) return NTT_ERR_ARG;  // before packing into p32[12] / g32[12]
-  if ((flags & NTT_PLAN_STOCKHAM) && (flags & NTT_PLAN_GZKP)) return NTT_ERR_ARG;  // one rival schedule per plan
-  if ((flags & NTT_PLAN_IN_PLACE) && (flags & (NTT_PLAN_STOCKHAM | NTT_PLAN_GZKP | NTT_PLAN_TWIDDLE_ONLY)))
+  const unsigned rivals = flags & (NTT_PLAN_STOCKHAM | NTT_PLAN_GZKP | NTT_PLAN_NAIVE);
+  if (rivals & (rivals - 1)) return NTT_ERR_ARG;  // one rival schedule per plan
+  if ((flags & NTT_PLAN_IN_PLACE) && (flags & (NTT_PLAN_STOCKHAM | NTT_PLAN_GZKP | NTT_PLAN_NAIVE | NTT_PLAN_TWIDDLE_ONLY)))
     return NTT_ERR_ARG;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return NTT_ERR_NODEV;

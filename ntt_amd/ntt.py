@@ -80,7 +80,7 @@ class NTTPlan:
     def __init__(self, field_id: int = 1, log_n: int = 10, limbs64: int = 4, device: int = 0,
                  modulus: Optional[int] = None, generator: Optional[int] = None, twiddle_only: bool = False,
                  montgomery_io: bool = False, stockham: bool = False, gzkp: bool = False,
-                 in_place: bool = False, single_launch: bool = False):
+                 in_place: bool = False, single_launch: bool = False, naive: bool = False):
         self._lib = _L.load()
         self.log_n = int(log_n)
         self.n = 1 << self.log_n
@@ -97,6 +97,8 @@ class NTTPlan:
         flags |= _L.NTT_PLAN_STOCKHAM if stockham else 0
         # gzkp: the reference's GZKP(B, G) rival schedule (bit reversal + in-place DIT passes)
         flags |= _L.NTT_PLAN_GZKP if gzkp else 0
+        # naive: the reference's `naive` rival (bit reversal + one radix-2 round per launch)
+        flags |= _L.NTT_PLAN_NAIVE if naive else 0
         # in_place: no plan scratch, palindromic passes + tile-swap digit reversal (the reference's
         # self-sort-in-place property, GZKP-NTT.cu:1359-1449; ntt.h NTT_PLAN_IN_PLACE)
         flags |= _L.NTT_PLAN_IN_PLACE if in_place else 0

@@ -124,3 +124,16 @@ def test_compiled_c_caller_builds_against_header_and_library():
         pytest.skip("gcc / ROCm headers unavailable")
     from tests.dropin_build import build
     assert os.access(build(), os.X_OK)
+
+
+def test_python_constants_match_the_header():
+    """Every NTT_PLAN_* / NTT_ERR_* / NTT_FIELD_* / NTT_OK value ntt_amd.lib mirrors equals the
+    header's #define, and every such #define is mirrored."""
+    from ntt_amd import lib as L
+    text = open(os.path.join(INCLUDE, "ntt.h")).read()
+    defs = {m.group(1): int(m.group(2)) for m in
+            re.finditer(r"^#define\s+(NTT_(?:PLAN|ERR|FIELD)_\w+|NTT_OK)\s+\(?(-?\d+)u?\)?", text, flags=re.M)}
+    assert "NTT_PLAN_NAIVE" in defs and "NTT_ERR_DEVICE" in defs
+    for name, value in defs.items():
+        assert hasattr(L, name), name
+        assert getattr(L, name) == value, (name, getattr(L, name), value)

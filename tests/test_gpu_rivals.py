@@ -4,7 +4,9 @@ BN254 / BLS12-381 Fr, and bit-for-bit agreement with the default four-step DIF s
 * "stockham": the bellperson / improved_NTT_v1..v4 family (GZKP-NTT.cu:324-386 FIELD_radix_fft,
   :556-1296) as Stockham autosort pass kernels (KIND_STOCKHAM, plan flag NTT_PLAN_STOCKHAM);
 * "gzkp": GZKP(B, G) (GZKP-NTT.cu:115-233; parallel-load.cu for P): bit reversal, then in-place DIT
-  passes with input twiddles (KIND_DIT, plan flag NTT_PLAN_GZKP)."""
+  passes with input twiddles (KIND_DIT, plan flag NTT_PLAN_GZKP);
+* "naive": the reference's `naive` (GZKP-NTT.cu:59-95, big-num.cu:67-170): bit reversal, then one
+  radix-2 DIT round per launch (k_naive_round, plan flag NTT_PLAN_NAIVE)."""
 import os
 
 import numpy as np
@@ -19,12 +21,13 @@ GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "ref_p469762049
 THREADS = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "8"))))
 
 
-RIVALS = ["stockham", "gzkp"]
+RIVALS = ["stockham", "gzkp", "naive"]
 
 
 def _plan(fid, log_n, L, sched):
     from ntt_amd.ntt import NTTPlan
-    return NTTPlan(field_id=fid, log_n=log_n, limbs64=L, stockham=sched == "stockham", gzkp=sched == "gzkp")
+    return NTTPlan(field_id=fid, log_n=log_n, limbs64=L, stockham=sched == "stockham", gzkp=sched == "gzkp",
+                   naive=sched == "naive")
 
 
 @pytest.mark.parametrize("sched", RIVALS)
@@ -75,5 +78,30 @@ def test_rival_2pow24_bn254_elementwise(sched):
 
 def test_rival_flags_are_exclusive():
     from ntt_amd.ntt import NTTPlan
-    with pytest.raises(Exception):
-        NTTPlan(field_id=1, log_n=12, limbs64=4, stockham=True, gzkp=True)
+    for kw in ({"stockham": True, "gzkp": True}, {"stockham": True, "naive": True}, {"gzkp": True, "naive": True},
+               {"naive": True, "in_place": True}):
+        with pytest.raises(Exception):
+            NTTPlan(field_id=1, log_n=12, limbs64=4, **kw)
+    with pytest.raises(Exception):  # the rivals cover P and the 4 x 64-bit layout
+        NTTPlan(field_id=2, log_n=12, limbs64=6, naive=True)
+
+
+@pytest.mark.parametrize("fid,L,log_n", [(0, 1, 1), (0, 1, 2), (0, 1, 5), (1, 4, 1), (1, 4, 3), (2, 4, 9)])
+def test_naive_small_sizes_vs_oracle(fid, L, log_n):
+    """The naive rival has no tile constraints: every size from 2 points, forward against the
+    oracle, the plan's (default-schedule) inverse back to the input; two launch groups recorded."""
+    p, g = R.FIELDS[fid]
+    pl = _plan(fid, log_n, L, "naive")
+    a = pl.fill(pl.empty(), "random", seed=7 + log_n)
+    x = a.cpu().numpy().view(np.uint64).reshape(-1, L).copy()
+    pl.set_profiling(True)
+    pl.forward(a)
+    assert len(pl.last_launch_ms()) == 2  # [bit reversal, the log2 n rounds]
+    pl.set_profiling(False)
+    got = a.cpu().numpy().view(np.uint64).reshape(-1, L)
+    if L == 1:
+        assert np.array_equal(got[:, 0].astype(np.int64), OC.ntt_u64(x[:, 0].astype(np.int64), p, g))
+    else:
+        assert np.array_equal(got, OC.ntt_mp(x, p, g))
+    pl.inverse(a)
+    assert np.array_equal(a.cpu().numpy().view(np.uint64).reshape(-1, L), x)

@@ -1,6 +1,7 @@
 """Default four-step DIF schedule vs the rival schedules (the reference's bellperson / improved_NTT
 family as Stockham autosort passes, NTT_PLAN_STOCKHAM; GZKP(B, G) as bit reversal + in-place DIT
-passes, NTT_PLAN_GZKP): forward transforms, inputs in HBM.
+passes, NTT_PLAN_GZKP; `naive` as bit reversal + one radix-2 round per launch, NTT_PLAN_NAIVE):
+forward transforms, inputs in HBM.
 
     python tools/bench_rivals.py [--out gpurun_out/rivals.jsonl]
 """
@@ -33,8 +34,8 @@ def main():
     from ntt_amd.ntt import NTTPlan
     rows = []
     for fid, L, lg in ((1, 4, 24), (1, 4, 20), (0, 1, 24), (0, 1, 26)):
-        for sched in ("default", "stockham", "gzkp"):
-            pl = NTTPlan(fid, lg, L, stockham=(sched == "stockham"), gzkp=(sched == "gzkp"))
+        for sched in ("default", "stockham", "gzkp", "naive"):
+            pl = NTTPlan(fid, lg, L, stockham=(sched == "stockham"), gzkp=(sched == "gzkp"), naive=(sched == "naive"))
             t = pl.fill(pl.empty(), "random", seed=1)
             pl.set_profiling(True)
             s = timeit(lambda: pl.forward(t))
@@ -42,6 +43,10 @@ def main():
             pl.set_profiling(False)
             r = {"field": fid, "limbs64": L, "log_n": lg, "schedule": sched, "passes": pl.passes, "ms": s * 1e3,
                  "elements_per_s": (1 << lg) / s, "launch_ms": launches}
+            if sched == "naive" and len(launches) == 2:  # [bit reversal, the log2 n rounds]
+                S = 8 * L
+                r["round_ms"] = launches[1] / lg
+                r["round_hbm_gbs"] = 2 * (1 << lg) * S / (r["round_ms"] * 1e-3) / 1e9  # one read + one write
             rows.append(r)
             print(json.dumps(r), flush=True)
             del pl, t

@@ -98,6 +98,9 @@ for s in $ARGS; do
         step wide0_$rep 200 env NTT_WIDE_TILES=0 python -u tools/exp_launches.py $C $L
         grep '^{' $O/wide0_$rep.log | sed "s/^/off /" >> $O/wide_ab.txt
       done ;;
+    naive)  # the reference's `naive` rival: parity, then its time against the default and the other rivals
+      step naive_tests 600 $PYT tests/test_gpu_rivals.py
+      step naive_bench 300 python -u tools/bench_rivals.py --out $O/rivals.jsonl ;;
     abmmc) step ab_mmc 600 tools/exp_variants.sh mmc ;;
     ptrace)  # C4 over 8 virtual ranks: kernel + copy traces of the piece schedules
       for c in 1,1 4,4 4,1 1,4; do
