@@ -130,3 +130,21 @@ def test_other_plans_keep_their_tiles():
     assert len(NTTPlan(1, 20, 4, in_place=True).passes) == 3
     assert len(NTTPlan(1, 20, 4, single_launch=True).passes) == 3
     assert len(NTTPlan(2, 20, 6).passes) == 3
+
+
+def test_custom_modulus_plan_and_256_bit_shim_take_the_two_pass_plan():
+    """ntt_plan_create_custom with a 4-limb modulus at 2^20 and the reference-shaped NTT_GZKP_256
+    shim (its cached plan) run the 4096-element tiles too, with the named plan's results."""
+    from ntt_amd.ntt import NTT_GZKP, NTTPlan
+    p, g = R.FIELDS[1]
+    named = NTTPlan(1, 20, 4)
+    custom = NTTPlan(log_n=20, limbs64=4, modulus=p, generator=g)
+    assert named.passes == custom.passes == [10, 10]
+    x = named.fill(named.empty(), "random", seed=41)
+    a, b, c = x.clone(), x.clone(), x.clone()
+    named.forward(a)
+    custom.forward(b)
+    NTT_GZKP(c.view(-1), 1 << 20, p, g)
+    assert torch.equal(a, b) and torch.equal(a, c)
+    custom.inverse(b)
+    assert torch.equal(b, x)
