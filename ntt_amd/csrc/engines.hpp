@@ -158,14 +158,23 @@ struct Eng29 {
   // limb-wise; K = (value bound of b) + 1 keeps the top limb non-negative when p_top >= 3.
   enum : int { PC_5_29 = 0, PC_9_30 = 1, PC_4_29 = 2, PC_17_29 = 3, PC_7_30 = 4 };
 
+  // The 256-bit class in the 48-B layout (W32 = 12) reads only the first 32 B of an element: its
+  // values (canonical inputs < p < 2^255, lazy intermediates < 2p) leave words 8..11 zero.  Holding
+  // 12 words per element in flight spilled 48 B per thread in pass 1 (12 B with 8 words).  The
+  // checked build reads all 48 B, so a non-canonical input still raises its flag.
   template <int MW = W32>
   __device__ static __forceinline__ void load(uint32_t (&x)[W], const uint32_t* __restrict__ base, size_t idx) {
+    constexpr int MR = (L <= 9 && MW > 8 && !NTT_DEBUG_CHECKS) ? 8 : MW;
     uint32_t w[MW];
     const uint4* p = reinterpret_cast<const uint4*>(base + idx * MW);
 #pragma unroll
     for (int q = 0; q < MW / 4; ++q) {
-      const uint4 v = p[q];
-      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+      if (4 * q < MR) {
+        const uint4 v = p[q];
+        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+      } else {
+        w[4 * q] = w[4 * q + 1] = w[4 * q + 2] = w[4 * q + 3] = 0u;
+      }
     }
     pack29<L, MW>(x, w);
   }

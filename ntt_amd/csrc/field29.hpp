@@ -397,8 +397,14 @@ F29_HD void pack29(uint32_t (&x)[L], const uint32_t (&w)[W32]) {
     const int bit = 29 * i, k = bit / 32, s = bit % 32;
     const uint32_t lo = (k < W32) ? w[k] : 0u;
     const uint32_t hi = (k + 1 < W32) ? w[k + 1] : 0u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // one v_alignbit per limb: the 64-bit form let the vectoriser read the words back through a
+    // stack copy at a one-word offset (48 B of scratch per thread in the 48-B layout's pass 1)
+    x[i] = __builtin_amdgcn_alignbit(hi, lo, (uint32_t)s) & kMask29;
+#else
     const uint64_t v = ((uint64_t)hi << 32) | lo;
     x[i] = (uint32_t)(v >> s) & kMask29;
+#endif
   }
 }
 // L normalised 29-bit limbs -> W32 little-endian 32-bit words (value must fit 32*W32 bits)

@@ -106,6 +106,15 @@ for s in $ARGS; do
     naive)  # the reference's `naive` rival: parity, then its time against the default and the other rivals
       step naive_tests 600 $PYT tests/test_gpu_rivals.py
       step naive_bench 300 python -u tools/bench_rivals.py --out $O/rivals.jsonl ;;
+    pack)  # pack29 with v_alignbit (no scratch copy) + 32-B reads of the 48-B layout, against the previous build
+      L="--warmup 50 --steps 100"
+      C="--cfg f2_L6_n24 --cfg f2_L6_n24_inv --cfg f2_L4_n24 --cfg f1_L4_n24 --cfg f1_L4_n20 --cfg f2_L6_n20"
+      for rep in 1 2; do
+        step packn_$rep 300 python -u tools/exp_launches.py $C $L
+        grep '^{' $O/packn_$rep.log | sed "s/^/new /" >> $O/pack_ab.txt
+        step packo_$rep 300 env NTT_LIB_PATH=ntt_amd/libntt_old.so python -u tools/exp_launches.py $C $L
+        grep '^{' $O/packo_$rep.log | sed "s/^/old /" >> $O/pack_ab.txt
+      done ;;
     abmmc) step ab_mmc 600 tools/exp_variants.sh mmc ;;
     ptrace)  # C4 over 8 virtual ranks: kernel + copy traces of the piece schedules
       for c in 1,1 4,4 4,1 1,4; do
