@@ -137,3 +137,17 @@ def test_python_constants_match_the_header():
     for name, value in defs.items():
         assert hasattr(L, name), name
         assert getattr(L, name) == value, (name, getattr(L, name), value)
+
+
+def test_conflicting_schedule_flags_are_rejected_without_a_device():
+    """One rival schedule per plan, and none with NTT_PLAN_IN_PLACE: refused before any device
+    query, so NTT_ERR_ARG here on a machine with no GPU."""
+    from ntt_amd import lib as L
+    so = L.load()
+    h = C.c_void_p()
+    rivals = (L.NTT_PLAN_STOCKHAM, L.NTT_PLAN_GZKP, L.NTT_PLAN_NAIVE)
+    bad = [a | b for i, a in enumerate(rivals) for b in rivals[i + 1:]]
+    bad += [r | L.NTT_PLAN_IN_PLACE for r in rivals] + [L.NTT_PLAN_IN_PLACE | L.NTT_PLAN_TWIDDLE_ONLY]
+    for flags in bad:
+        assert so.ntt_plan_create_ex(C.byref(h), 1, 12, 4, 0, flags) == L.NTT_ERR_ARG, flags
+        assert not h.value
