@@ -185,14 +185,27 @@ def _free_port() -> int:
         return so.getsockname()[1]
 
 
+def visible_devices() -> int:
+    """Devices the HIP runtime would show, counted in a CHILD process, so that the launcher parent
+    (spawn_ranks) never loads torch or the HIP runtime at all (the guarantee "no GPU call
+    before the launcher" must not rest on what device_count() happens to do on one image)."""
+    import subprocess
+    code = "import torch; print(torch.cuda.device_count())"
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return 0
+
+
 def spawn_ranks(args) -> int:
     """``python bench.py --gpus N`` with no launcher: start the N ranks as children through
-    torch.distributed.run (one process per GPU), before this process makes any GPU call, and return
-    their exit status.  rank 0's JSON line reaches our stdout through the inherited file descriptor."""
+    torch.distributed.run (one process per GPU) and return their exit status.  This process makes no
+    GPU call and does not import torch (visible_devices counts in a child).  rank 0's JSON line reaches
+    our stdout through the inherited file descriptor."""
     import subprocess
-    import torch  # device_count() does not initialise the GPU on this image
     rehearsal = os.environ.get("NTT_BENCH_EXCHANGE", "") == "host"
-    visible = torch.cuda.device_count()
+    visible = visible_devices()
     if args.gpus > visible and not rehearsal:
         print(f"bench.py: --gpus {args.gpus} but only {visible} visible device(s); refusing to run "
               f"{args.gpus} ranks on fewer GPUs (NTT_BENCH_EXCHANGE=host rehearses them on one GPU)",
@@ -510,8 +523,12 @@ def main():
                   ("u384 mod p: 14 x 29-bit limbs, u32 x u32 + u64 MAD" if args.limbs == 6 else
                    "u32 mod p (Montgomery)")),
         "data": "synthetic: SplitMix64 field elements (SURVEY §8d vector B, seed 2), resident in HBM",
+        # the plan's default schedule ping-pongs through an n-element plan scratch (the caller's buffer
+        # holds input and output); NTT_PLAN_IN_PLACE is the scratch-free contract of the reference's
+        # SSIP (GZKP-NTT.cu:1452-1558), timed in tools/bench_configs.py
         "config": {"workload": f"2^{args.log_n}-point {what} NTT, "
-                               f"{FIELD_NAMES[args.field]}, {args.limbs}x64-bit limbs, natural order, in place",
+                               f"{FIELD_NAMES[args.field]}, {args.limbs}x64-bit limbs, natural order, result in "
+                               f"the caller's buffer (passes ping-pong through an n-element plan scratch)",
                    "log_n": args.log_n, "field": FIELD_NAMES[args.field], "limbs64": args.limbs,
                    "passes_log_radix": passes,
                    "parallelism": ((f"REHEARSAL: four-step over {world} ranks on {ndev} GPU(s), host-staged "
@@ -539,6 +556,11 @@ def main():
         out["exchange_bytes_per_peer"] = peer_bytes
         out["exchange_gbps_per_link"] = (peer_bytes / (exchange_ms * 1e-3) / 1e9
                                          if exchange_ms and world > 1 else None)
+        # the convention, comparable with DESIGN §6's 77 / 153 GB/s per direction: ONE direction of one
+        # peer pair's link -- the block a rank sends one peer per exchange over the window; the same
+        # amount flows the other way at the same time
+        out["exchange_gbps_convention"] = ("per direction: exchange_bytes_per_peer (sent to ONE peer) / exchange_ms; "
+                                           "the peer sends as much back over the same link concurrently")
         if rehearsal:
             out["exchange_note"] = "host-staged gloo exchange on one GPU: not an xGMI link rate"
     # ---- SURVEY §8(d) roofline of the whole transform: 2 n S algorithmic bytes per transform
@@ -546,11 +568,15 @@ def main():
     alg_transform = 2 * n * elem_bytes
     t_transform = ms_per_step * 1e-3  # every rank runs its transform(s) per step
     achieved = alg_transform / t_transform / gpus_per_transform / 1e9
-    tag = f"f{args.field}_L{args.limbs}_n{args.log_n}_w{gpus_per_transform}{'_inv' if args.inverse else ''}"
-    launch_bytes, prof_src = load_traffic(tag) if not four_step else (None, "four-step: not profiled")
+    # PMC entries: one GPU's transform (tag ..._w1), or one RANK's local launches of the four-step over
+    # G ranks (tag ..._w<G>_fs: rank 0 of a G-rank plan on one GPU, rows + columns, tools/pmc_ranklocal.sh;
+    # kernels only -- the all-to-all's own HBM reads and writes are not in it)
+    tag = (f"f{args.field}_L{args.limbs}_n{args.log_n}_w{gpus_per_transform}{'_fs' if four_step else ''}"
+           f"{'_inv' if args.inverse else ''}")
+    launch_bytes, prof_src = load_traffic(tag)
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
-            "traffic": (sum(launch_bytes) / gpus_per_transform if launch_bytes else None),
+            "traffic": (sum(launch_bytes) if launch_bytes else None),
             "traffic_source": prof_src,
             "algorithmic_bytes": alg_transform / gpus_per_transform,
             "definition": "SURVEY §8(d): 2·n·S bytes per transform (one read + one write of the vector) "

@@ -124,6 +124,15 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
  * plan's other calls run the default schedule.  Exclusive with the other rivals and with
  * NTT_PLAN_IN_PLACE. */
 #define NTT_PLAN_NAIVE 64u
+/* Rival schedule, the reference's `naive_no_swap` (GZKP-NTT.cu:237-296; its main checks it against
+ * the CPU NTT, GZKP-NTT.cu:1653-1660): a radix-2 Stockham autosort -- log2 n rounds of one launch
+ * each, round s reading x[i], x[i + n/2] and writing y[2i - k], y[2i - k + 2^s] (k = i mod 2^s,
+ * w = w_n^(k n / 2^(s+1)) from the n/2-entry power table), ping-pong between the caller's buffer and
+ * a plan buffer, natural order in and out, no bit reversal.  When log2 n is odd the last round lands
+ * in the plan buffer and one device copy brings it back.  Forward single transforms of P469762049 and
+ * 4-limb plans; the plan's other calls run the default schedule.  Exclusive with the other rivals and
+ * with NTT_PLAN_IN_PLACE. */
+#define NTT_PLAN_NO_SWAP 128u
 int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags);
 /* Device-side status of a plan (blocking: synchronises the device, then reads and clears it).
  * *bad bit 0: an inter-workgroup wait gave up at its watchdog (NTT_PLAN_SINGLE_LAUNCH, or the fused

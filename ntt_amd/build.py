@@ -32,6 +32,7 @@ INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
 # slowest translation units first (the pool runs them in list order)
 SOURCES = ["ntt_e256_fused.hip"]  # the fused single-launch 3-pass schedule (NTT_PLAN_SINGLE_LAUNCH)
+SOURCES += ["ntt_e256t_fused.hip"]  # the two-pass single launch on 4096-element tiles (2^20)
 SOURCES += [f"ntt_{e}_{k}.hip" for e in ("e384", "e256", "e256w", "ep") for k in ("col", "single", "fin", "misc")]
 SOURCES += ["ntt_e256_stk.hip", "ntt_ep_stk.hip"]  # the bellperson-family rival schedule (NTT_PLAN_STOCKHAM)
 SOURCES += ["ntt_e256_dit.hip", "ntt_ep_dit.hip"]  # the GZKP(B, G) rival schedule (NTT_PLAN_GZKP)

@@ -26,6 +26,9 @@ int plan_build_fs_table(ntt_plan* plan, void* table, unsigned log_rows, unsigned
                         uint64_t col0, bool inverse, hipStream_t st);
 size_t plan_table_entry_bytes(const ntt_plan* plan);
 int plan_device(const ntt_plan* plan);
+// A plan for the library's own callers (the rank plan's row / column transforms, which run only
+// through plan_run_fs): no second plan of 4096-element tiles (make_wide_plan).
+int plan_create_internal(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device);
 // pass kernels that a 2^log_x-point transform takes with this plan's engine (the four-step split)
 unsigned plan_passes_for(const ntt_plan* plan, unsigned log_x);
 

@@ -154,7 +154,9 @@ struct FusedArgs {
                                // output), bit 2 static tile order (needs every workgroup resident)
   uint32_t mode;               // 0: dataflow hand-offs between tiles (k_fused3); 1: two grid barriers
                                // over a cooperative launch (k_fused3b); 2: the NTT_PLAN_IN_PLACE form,
-                               // three grid barriers, one workgroup per tile (k_fused3bi)
+                               // three grid barriers, one workgroup per tile (k_fused3bi); 3: two passes
+                               // on 4096-element tiles, one barrier (k_fused2b); 4: the same in place,
+                               // two barriers (k_fused2bi)
   Watchdog wd;                 // bounded waits
   uint32_t* shards;            // grid barriers (modes 1, 2): 8 arrival shards, one 128-B line each
 };
@@ -166,6 +168,19 @@ hipError_t launch_fused3(int r1, int r2, int r3, const uint32_t* src, uint32_t* 
 // `device` (occupancy query x CUs)
 template <class E>
 hipError_t fused3_capacity(int r1, int r2, int r3, int device, uint32_t* wgs, uint32_t mode = 0);
+
+// The two-pass single launch on 4096-element tiles (k_fused2b, FusedArgs::mode 3; in place:
+// k_fused2bi, mode 4): 2^20 = 10 + 10 on Eng256T with one grid barrier, a plain launch
+// the engines k_fused2b / k_fused2bi are instantiated for (radices 10 + 10: 2^20 on 4096-element tiles)
+template <class E>
+__host__ __device__ constexpr bool fused2_engine() {
+  return E::FASTRED && !E::LDS_TW && E::TILE_LOG == 12 && E::EPT == 4 && E::W == 9 && E::MEMW == 8;
+}
+template <class E>
+hipError_t launch_fused2(int r1, int r2, const uint32_t* src, uint32_t* scratch, uint32_t* dst, const PassArgs<E>& A1,
+                         const PassArgs<E>& A2, const FusedArgs& F, hipStream_t st);
+template <class E>
+hipError_t fused2_capacity(int r1, int r2, int device, uint32_t* wgs, uint32_t mode);
 
 // The in-place final pass with the digit reversal fused (NTT_PLAN_IN_PLACE, batch 1): A.ipn_* set,
 // grid = n / TILE workgroups, src == dst.  See k_final_ipn.
@@ -196,6 +211,10 @@ hipError_t launch_build_tw_sh(uint32_t* out, size_t count, uint32_t log_r, uint3
 template <class E>
 hipError_t launch_build_pow(uint32_t* out, size_t count, const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits,
                             const typename E::Args& F, hipStream_t st);
+// NTT_PLAN_NO_SWAP: one radix-2 Stockham round (stride 2^log_s) of the reference's `naive_no_swap`
+template <class E>
+hipError_t launch_noswap_round(const uint32_t* src, uint32_t* dst, uint32_t log_n, uint32_t log_s, const uint32_t* pw,
+                               const typename E::Args& F, hipStream_t st);
 template <class E>
 hipError_t launch_naive_round(const uint32_t* src, uint32_t* dst, uint32_t log_n, uint32_t log_s, const uint32_t* pw,
                               const typename E::Args& F, hipStream_t st);

@@ -392,11 +392,12 @@ __device__ __forceinline__ bool grid_barrier_words(uint32_t* top, uint32_t* shar
   __syncthreads();
   return __builtin_amdgcn_readfirstlane(s_ok) != 0u;
 }
-// The in-place single launch's third barrier, between every final tile's loads and any store
-// (PassArgs: ipn_sync = the top counter, ipn_shards = the shard lines, ipn_go = the go word)
-template <class E>
+// The in-place single launch's last barrier (the K-th of the launch: 3 in k_fused3bi, 2 in
+// k_fused2bi), between every final tile's loads and any store (PassArgs: ipn_sync = the top counter,
+// ipn_shards = the shard lines, ipn_go = the go word)
+template <uint32_t K, class E>
 __device__ __forceinline__ bool ipn_grid_barrier(const PassArgs<E>& A) {
-  return grid_barrier_words(A.ipn_sync, A.ipn_shards, A.ipn_go, 3u, A.wd);
+  return grid_barrier_words(A.ipn_sync, A.ipn_shards, A.ipn_go, K, A.wd);
 }
 
 // LDS of one pass tile (words), and whether the pass stages its w_R^e table in LDS: E::LDS_TW
@@ -648,8 +649,8 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
   // ------------------------------------------------------------------ output
   if constexpr (IPN == 1) {  // the slab this tile writes into has been read (or the wait gave up: no stores)
     if (!ipn_wait_mirror(A, midrev)) return;
-  } else if constexpr (IPN == 2) {  // in-place single launch: every final tile has read (grid barrier)
-    if (!ipn_grid_barrier(A)) return;
+  } else if constexpr (IPN >= 2) {  // in-place single launch: every final tile has read (grid barrier)
+    if (!ipn_grid_barrier<IPN == 2 ? 3u : 2u>(A)) return;
   }
 #if NTT_PRIO & 2
   __builtin_amdgcn_s_setprio(1);  // timing experiment: finishing tiles drain first
@@ -1109,6 +1110,119 @@ void k_fused3bi(const FusedKArgs<E> K) {
   }
 }
 
+// BASELINE config 2 as ONE kernel on 4096-element tiles (the reference's 2^20
+// schedule is 4 launches, GZKP-NTT.cu:1509-1545): the two passes (10 + 10) of Eng256T with ONE grid
+// barrier between them.  2^20 is 256 tiles per pass, one 1024-thread workgroup per CU, so each
+// workgroup runs one tile of each pass.  A plain launch (no cooperative launch: its ~20 us per call
+// was most of the 3-pass single launch's deficit) of at most the occupancy query's
+// workgroups; the barrier is bounded (Watchdog), so a device shared with another persistent kernel
+// ends in NTT_ERR_DEVICE, never a hang.
+//   k_fused2b  (FusedArgs::mode 3): pass 1 caller -> scratch (write-through), barrier, final pass
+//              scratch -> caller, natural order.
+//   k_fused2bi (FusedArgs::mode 4): NTT_PLAN_IN_PLACE, the palindromic 10 + 10: pass 1 in place,
+//              barrier 1, the final pass loads and transforms every tile, barrier 2 (every tile has
+//              read: all 256 final tiles are resident), then the stores to the natural positions in the
+//              mirror slab (pass_tile IPN = 3).  No scratch.
+template <class E, int R1, int R2>
+__global__ __launch_bounds__((1 << E::TILE_LOG) / E::EPT) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
+void k_fused2b(const FusedKArgs<E> K) {
+  static_assert(E::FASTRED && !E::LDS_TW, "fused schedule: FAST 256-bit engines");
+  constexpr int LW = pass_lds_words<E, R1, KIND_COLUMN>();
+  static_assert(LW == pass_lds_words<E, R2, KIND_FINAL>(), "one tile size");
+  __shared__ __attribute__((aligned(16))) uint32_t lds[LW];
+  __shared__ uint32_t lds_tw[1];
+  const FusedArgs& F = K.F;
+  const uint32_t G = gridDim.x;
+  for (uint32_t w = blockIdx.x; w < F.tiles; w += G) {  // pass 1: the caller's buffer -> scratch
+    const FusedKArgs<E>& L = fused_kargs<E>();
+    pass_tile<E, R1, KIND_COLUMN, true, true, PRO_NONE, true, 0, false, true, true>(L.src, L.scratch, L.A1, w, 0, lds,
+                                                                                      lds_tw);
+    __syncthreads();
+  }
+  const bool ok = fused_grid_barrier(F, 1);
+  for (uint32_t w = blockIdx.x; ok && w < F.tiles; w += G) {  // final pass: scratch -> the caller's buffer
+    const FusedKArgs<E>& L = fused_kargs<E>();
+    pass_tile<E, R2, KIND_FINAL, false, true, PRO_NONE, true, 0, false, false, true>(L.scratch, L.dst, L.A3, w, 0, lds,
+                                                                                      lds_tw);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0 && __hip_atomic_fetch_add(F.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
+    // the last workgroup out: every other one has passed (or given up at) the barrier
+    __hip_atomic_store(F.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(F.sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (F.wd.abort) __hip_atomic_store(F.wd.abort, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(F.sync + F.rbase, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t sh = 0; sh < 8; ++sh) __hip_atomic_store(F.shards + 32 * sh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <class E, int R>
+__global__ __launch_bounds__((1 << E::TILE_LOG) / E::EPT) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
+void k_fused2bi(const FusedKArgs<E> K) {
+  static_assert(E::FASTRED && !E::LDS_TW && E::SCRW == E::MEMW, "fused in place: 256-bit engines");
+  constexpr int LW = pass_lds_words<E, R, KIND_COLUMN>();
+  static_assert(LW == pass_lds_words<E, R, KIND_FINAL>(), "one tile size");
+  __shared__ __attribute__((aligned(16))) uint32_t lds[LW];
+  __shared__ uint32_t lds_tw[1];
+  const FusedArgs& F = K.F;
+  const uint32_t G = gridDim.x;
+  for (uint32_t w = blockIdx.x; w < F.tiles; w += G) {  // pass 1, in place
+    const FusedKArgs<E>& L = fused_kargs<E>();
+    pass_tile<E, R, KIND_COLUMN, true, true, PRO_NONE, true, 0, false, true, true>(L.dst, L.dst, L.A1, w, 0, lds,
+                                                                                     lds_tw);
+    __syncthreads();
+  }
+  const bool ok = fused_grid_barrier(F, 1);
+  if (ok && blockIdx.x < F.tiles) {  // final pass: load, transform, barrier 2 (inside), natural-order stores
+    const FusedKArgs<E>& L = fused_kargs<E>();
+    pass_tile<E, R, KIND_FINAL, false, true, PRO_NONE, true, 0, false, false, true, 3>(L.dst, L.dst, L.A3, blockIdx.x, 0,
+                                                                                        lds, lds_tw);
+  }
+  if (threadIdx.x == 0 && __hip_atomic_fetch_add(F.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
+    __hip_atomic_store(F.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(F.sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (F.wd.abort) __hip_atomic_store(F.wd.abort, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t k = 0; k < 2; ++k)
+      __hip_atomic_store(F.sync + F.rbase + 32 * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t sh = 0; sh < 8; ++sh) __hip_atomic_store(F.shards + 32 * sh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <class E>
+hipError_t launch_fused2(int r1, int r2, const uint32_t* src, uint32_t* scratch, uint32_t* dst, const PassArgs<E>& A1,
+                         const PassArgs<E>& A2, const FusedArgs& F, hipStream_t st) {
+  if constexpr (!fused2_engine<E>()) {
+    return hipErrorInvalidValue;
+  } else {
+    if (r1 != 10 || r2 != 10 || (F.mode != 3 && F.mode != 4)) return hipErrorInvalidValue;
+    const dim3 g(F.nwg), b((1 << E::TILE_LOG) / E::EPT);
+    FusedKArgs<E> K{src, scratch, dst, A1, A1, A2, F};
+    if (F.mode == 4)
+      hipLaunchKernelGGL((k_fused2bi<E, 10>), g, b, 0, st, K);
+    else
+      hipLaunchKernelGGL((k_fused2b<E, 10, 10>), g, b, 0, st, K);
+    return hipGetLastError();
+  }
+}
+// workgroups of k_fused2b (mode 3) / k_fused2bi (mode 4) resident at once on `device`
+template <class E>
+hipError_t fused2_capacity(int r1, int r2, int device, uint32_t* wgs, uint32_t mode) {
+  if constexpr (!fused2_engine<E>()) {
+    return hipErrorInvalidValue;
+  } else {
+    if (r1 != 10 || r2 != 10) return hipErrorInvalidValue;
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return hipErrorInvalidValue;
+    const int threads = (1 << E::TILE_LOG) / E::EPT;
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per, mode == 4 ? reinterpret_cast<const void*>(&k_fused2bi<E, 10>) : reinterpret_cast<const void*>(&k_fused2b<E, 10, 10>),
+        threads, 0);
+    if (e != hipSuccess) return e;
+    *wgs = (uint32_t)(cus * per);
+    return hipSuccess;
+  }
+}
+
 template <class E>
 hipError_t launch_fused3(int r1, int r2, int r3, const uint32_t* src, uint32_t* scratch, uint32_t* dst,
                          const PassArgs<E>& A1, const PassArgs<E>& A2, const PassArgs<E>& A3, const FusedArgs& F,
@@ -1301,9 +1415,11 @@ hipError_t launch_build_pow(uint32_t* out, size_t count, const uint32_t* lo, con
 // pos = 2 (id - off) + off and pos + s (s = 2^log_s, off = id mod s) as (a + w b, a - w b) with
 // w = w_n^(off n / 2s) -- the reference kernel's indexing (GZKP-NTT.cu:59-71), one thread per
 // butterfly, canonical in and out (the product through the element-format power table: mulv).
-// HBM-bound by construction: every round reads and writes the whole vector.
+// HBM-bound by construction: every round reads and writes the whole vector.  src and dst alias (every
+// round but the last runs in place), so neither is __restrict__: each thread reads its two
+// elements before it writes them, and no other thread touches them in the round.
 template <class E>
-__global__ void k_naive_round(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t log_n,
+__global__ void k_naive_round(const uint32_t* src, uint32_t* dst, uint32_t log_n,
                               uint32_t log_s, const uint32_t* __restrict__ pw, const typename E::Args F) {
   const size_t half = size_t(1) << (log_n - 1), s = size_t(1) << log_s;
   NTT_GRID_STRIDE(id, half) {
@@ -1317,6 +1433,37 @@ __global__ void k_naive_round(const uint32_t* __restrict__ src, uint32_t* __rest
     E::template store<2 * E::IN>(dst, pos, a, F);
     E::template store<2 * E::IN>(dst, pos + s, b, F);
   }
+}
+
+// One radix-2 round of the `naive_no_swap` rival (GZKP-NTT.cu:237-258): butterfly i < n/2 reads
+// x[i] and x[i + n/2], multiplies the second by w = w_n^(k n / 2s) (k = i mod s, s = 2^log_s: the
+// reference's roots[k * (len / (stride << 1))]) and writes a + w b to y[2i - k], a - w b to
+// y[2i - k + s] -- a radix-2 Stockham autosort: natural order in and out after log2 n rounds.
+// src != dst (ping-pong).  HBM-bound by construction, like k_naive_round.
+template <class E>
+__global__ void k_noswap_round(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t log_n,
+                               uint32_t log_s, const uint32_t* __restrict__ pw, const typename E::Args F) {
+  const size_t half = size_t(1) << (log_n - 1), s = size_t(1) << log_s;
+  NTT_GRID_STRIDE(i, half) {
+    const size_t k = i & (s - 1), j = (i << 1) - k;
+    uint32_t a[E::W], b[E::W], w[E::W];
+    E::load(a, src, i);
+    E::load(b, src, i + half);
+    E::template load<E::TABW>(w, pw, k << (log_n - 1 - log_s));
+    E::mulv(b, w, F);  // w R_e: the Montgomery product leaves w b
+    E::template bfly_l<E::IN>(a, b, F);
+    E::template store<2 * E::IN>(dst, j, a, F);
+    E::template store<2 * E::IN>(dst, j + s, b, F);
+  }
+}
+
+template <class E>
+hipError_t launch_noswap_round(const uint32_t* src, uint32_t* dst, uint32_t log_n, uint32_t log_s, const uint32_t* pw,
+                               const typename E::Args& F, hipStream_t st) {
+  if (log_n == 0 || log_s >= log_n || src == dst) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((k_noswap_round<E>), dim3(grid_1d(size_t(1) << (log_n - 1))), dim3(256), 0, st, src, dst, log_n,
+                     log_s, pw, F);
+  return hipGetLastError();
 }
 
 template <class E>
@@ -1941,6 +2088,11 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
                                        const PassArgs<E>&, const PassArgs<E>&, const FusedArgs&, hipStream_t);      \
   template hipError_t fused3_capacity<E>(int, int, int, int, uint32_t*, uint32_t);
 
+#define NTT_INSTANTIATE_FUSED2(E)                                                                                 \
+  template hipError_t launch_fused2<E>(int, int, const uint32_t*, uint32_t*, uint32_t*, const PassArgs<E>&,           \
+                                       const PassArgs<E>&, const FusedArgs&, hipStream_t);                          \
+  template hipError_t fused2_capacity<E>(int, int, int, uint32_t*, uint32_t);
+
 #define NTT_INSTANTIATE(E)                                                                                         \
   NTT_EXTERN_KIND(E, KIND_COLUMN)                                                                                  \
   NTT_EXTERN_KIND(E, KIND_FINAL)                                                                                   \
@@ -1980,6 +2132,8 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
   template hipError_t launch_build_pow<E>(uint32_t*, size_t, const uint32_t*, const uint32_t*, uint32_t,           \
                                           const typename E::Args&, hipStream_t);                                   \
   template hipError_t launch_naive_round<E>(const uint32_t*, uint32_t*, uint32_t, uint32_t, const uint32_t*,       \
-                                            const typename E::Args&, hipStream_t);
+                                            const typename E::Args&, hipStream_t);                                 \
+  template hipError_t launch_noswap_round<E>(const uint32_t*, uint32_t*, uint32_t, uint32_t, const uint32_t*,      \
+                                             const typename E::Args&, hipStream_t);
 
 }  // namespace ntt

@@ -133,6 +133,9 @@ struct PlanBase {
   virtual int coset(void* d, const uint64_t* shift, unsigned limbs64, bool inverse, hipStream_t st) = 0;
   virtual int count_noncanonical(const void* d, uint64_t count, uint64_t* bad, hipStream_t st) = 0;
   virtual int device_status(unsigned* bad) = 0;
+  // the plan's batch-1 forward / inverse run as ONE launch (NTT_PLAN_SINGLE_LAUNCH): its single-launch
+  // state is built now (a second plan of 4096-element tiles is kept only when this holds)
+  virtual bool single_launch_ready() { return false; }
   uint64_t n = 0;
   unsigned flags = 0;
   unsigned log_n = 0, elem_bytes = 0, npass = 0;
@@ -476,6 +479,7 @@ struct PlanImpl final : PlanBase {
     if (d_coset_full) (void)hipFree(d_coset_full);
     if (d_sync) (void)hipFree(d_sync);
     if (d_sync_ip) (void)hipFree(d_sync_ip);
+    if (d_sync2) (void)hipFree(d_sync2);
     if (d_ipn) (void)hipFree(d_ipn);
     if (d_pw) (void)hipFree(d_pw);
     if (d_dbg) (void)hipFree(d_dbg);
@@ -665,7 +669,7 @@ struct PlanImpl final : PlanBase {
     // NTT_PLAN_GZKP runs on the same per-pass tables: Stockham pass i's w_n^((k pi) << (log_n - lgp_i - r_i))
     // for k < 2^lgp_i is the GZKP DIT pass's w_N^(c d), N = 2^(lgp_i + r_i)
     if (rc == NTT_OK && (flags & (NTT_PLAN_STOCKHAM | NTT_PLAN_GZKP))) rc = build_stockham();
-    if (rc == NTT_OK && (flags & NTT_PLAN_NAIVE)) rc = build_naive();
+    if (rc == NTT_OK && (flags & (NTT_PLAN_NAIVE | NTT_PLAN_NO_SWAP))) rc = build_naive();
     (void)hipSetDevice(cur);
     return rc;
   }
@@ -780,6 +784,22 @@ struct PlanImpl final : PlanBase {
     return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
   }
 
+  // NTT_PLAN_NO_SWAP (rival schedule, the reference's `naive_no_swap`, GZKP-NTT.cu:237-296): a radix-2
+  // Stockham autosort, one launch per round, ping-pong between the caller's buffer and the plan
+  // buffer (natural order in and out, no bit reversal); an odd round count ends in the plan buffer
+  // and one device copy brings it back.  The same n/2-entry power table as NTT_PLAN_NAIVE.
+  int run_noswap(uint32_t* data, hipStream_t st) {
+    begin(st);
+    hipError_t e = hipSuccess;
+    uint32_t* buf[2] = {data, d_naive_buf};
+    for (unsigned s = 0; s < log_n && e == hipSuccess; ++s)
+      e = launch_noswap_round<E>(buf[s & 1], buf[(s + 1) & 1], log_n, s, d_naive_pw, Ff, st);
+    if (e == hipSuccess && (log_n & 1))
+      e = hipMemcpyAsync(data, d_naive_buf, (size_t)n * MEMW * 4, hipMemcpyDeviceToDevice, st);
+    mark(st);  // last_launch_ms: [all rounds (and the copy)]
+    return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+  }
+
   int run_stockham(const uint32_t* in, uint32_t* out, hipStream_t st) {
     const uint32_t grid = (uint32_t)(n >> tile_log_of<E>());
     hipError_t e = hipSuccess;
@@ -845,8 +865,16 @@ struct PlanImpl final : PlanBase {
       const uint32_t* hi = d_tab + (dir ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
       // column-group-major layout of the pass kernel's tiles (T = TILE / R columns per workgroup)
       if (launch_build_tw<E>(d_fulls[dir] + full_off[i] * TABW, 1ull << blk, r[i], tile_log_of<E>() - r[i], log_n - blk,
-                             lo, hi, lo_bits, dir ? Fi : Ff, st) != hipSuccess)
-        return NTT_ERR_HIP;
+                             lo, hi, lo_bits, dir ? Fi : Ff, st) != hipSuccess) {
+        // a partly built table must never be read as a built one: drop it; the
+        // direction falls back to the two-level tables (the inverse) or the plan fails (creation)
+        (void)hipFree(d_fulls[dir]);
+        d_fulls[dir] = nullptr;
+        (void)hipGetLastError();
+        if (dir == 0) return NTT_ERR_HIP;
+        full_failed[dir] = true;
+        return NTT_OK;
+      }
       blk -= r[i];
     }
     return NTT_OK;
@@ -1071,6 +1099,8 @@ struct PlanImpl final : PlanBase {
       return run_gzkp(static_cast<uint32_t*>(d), static_cast<uint32_t*>(d), st);
     if ((flags & NTT_PLAN_NAIVE) && !inverse && batch == 1 && d_naive_pw)
       return run_naive(static_cast<uint32_t*>(d), static_cast<uint32_t*>(d), st);
+    if ((flags & NTT_PLAN_NO_SWAP) && !inverse && batch == 1 && d_naive_pw)
+      return run_noswap(static_cast<uint32_t*>(d), st);
     return run_io(static_cast<uint32_t*>(d), nullptr, static_cast<uint32_t*>(d), batch, inverse, st);
   }
 
@@ -1191,6 +1221,25 @@ struct PlanImpl final : PlanBase {
           const unsigned run_bytes = (1u << (tile_log_of<E>() - r[i])) * SCRW * 4;
           if (xcd_order == 1 || (i > 0 && run_bytes < 128)) PA[i].flags |= 4u;
         }
+      if constexpr (fused2_engine<E>()) {  // 2^20 on 4096-element tiles: the two-pass single launch
+        if (!io && batch == 1 && npass == 2 && fused_enabled() && fused2_ready(PA, inplace)) {
+          FusedArgs F = inplace ? fargs2_ip : fargs2;
+          F.wd = watchdog(F.wd.abort);
+          if (inplace) {  // k_fused2bi: the final pass's barrier is the launch's second
+            PassArgs<E> B = A;
+            B.flags &= ~2u;
+            B.ipn_sync = F.sync;
+            B.ipn_go = F.sync + F.rbase + 32;
+            B.ipn_shards = F.shards;
+            B.wd = F.wd;
+            e = launch_fused2<E>((int)r[0], (int)r[1], out, nullptr, out, PA[0], B, F, st);
+          } else {
+            e = launch_fused2<E>((int)r[0], (int)r[1], in, work, out, PA[0], A, F, st);
+          }
+          mark(st);
+          return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+        }
+      }
       if constexpr (std::is_same_v<E, Eng256>) {  // the engine k_fused3 is instantiated for
         if (!io && !inplace && batch == 1 && fused_enabled() && fused_ready(PA)) {
           // one persistent launch for the three passes (NTT_PLAN_SINGLE_LAUNCH, k_fused3)
@@ -1327,6 +1376,63 @@ struct PlanImpl final : PlanBase {
     }
   }
   const FusedArgs& fused_args() const { return fargs; }
+
+  // ---- the two-pass single launch on 4096-element tiles (NTT_PLAN_SINGLE_LAUNCH, 2^20 4-limb plans:
+  // k_fused2b, and k_fused2bi in place; ntt_kernels_impl.hpp).  Plain launches of at most the occupancy
+  // query's workgroups; the in-place form needs every one of the 256 final tiles resident.
+  // Sync words: [0] top arrivals, [1] exits; go words at 32, 64; abort at 96; shards at 128 + 32 s.
+  uint32_t* d_sync2 = nullptr;
+  FusedArgs fargs2{}, fargs2_ip{};
+  int fused2_state[2] = {0, 0};  // [in place]: 0 not built, 1 ready, -1 unavailable
+  bool fused2_ready(const PassArgs<E>* PA, bool inplace) {
+    int& st = fused2_state[inplace ? 1 : 0];
+    if (st == 0) st = build_fused2(inplace) ? 1 : -1;
+    return st > 0 && PA[0].tw_full && !PA[0].tw_sh && !PA[0].src2 && !PA[0].tw_in;
+  }
+  bool build_fused2(bool inplace) {
+    if constexpr (!fused2_engine<E>()) {
+      return false;
+    } else {
+      if (npass != 2 || r[0] != 10 || r[1] != 10 || !use_full || !Ff.red_ok) return false;
+      if (!alloc_watch()) return false;
+      const uint32_t tiles = (uint32_t)(n >> tile_log_of<E>()), mode = inplace ? 4u : 3u;
+      uint32_t cap = 0;
+      if (fused2_capacity<E>((int)r[0], (int)r[1], device, &cap, mode) != hipSuccess || cap == 0) return false;
+      if (inplace && cap < tiles) return false;
+      if (!d_sync2) {
+        if (hipMalloc(&d_sync2, 384 * 4) != hipSuccess) {
+          d_sync2 = nullptr;
+          (void)hipGetLastError();
+          return false;
+        }
+        if (hipMemset(d_sync2, 0, 384 * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return false;
+      }
+      FusedArgs F{};
+      F.tiles = tiles;
+      F.nwg = inplace ? tiles : (tiles < cap ? tiles : cap);
+      F.mode = mode;
+      F.rbase = 32;
+      F.sync = d_sync2;
+      F.wd.abort = d_sync2 + 96;
+      F.shards = d_sync2 + 128;
+      if (getenv("NTT_FUSED_VERBOSE"))
+        fprintf(stderr, "libntt: two-pass single launch (mode %u), %u tiles per pass, %u workgroups (capacity %u)\n",
+                mode, tiles, F.nwg, cap);
+      (inplace ? fargs2_ip : fargs2) = F;
+      return true;
+    }
+  }
+  bool single_launch_ready() override {
+    if constexpr (!fused2_engine<E>()) {
+      return false;
+    } else {
+      const bool inplace = (flags & NTT_PLAN_IN_PLACE) != 0;
+      if (ensure_full(0, nullptr) != NTT_OK || !d_fulls[0]) return false;
+      int& st = fused2_state[inplace ? 1 : 0];
+      if (st == 0) st = build_fused2(inplace) ? 1 : -1;
+      return st > 0;
+    }
+  }
 
   // ---- the in-place single launch (NTT_PLAN_SINGLE_LAUNCH on an NTT_PLAN_IN_PLACE plan, k_fused3bi):
   // 3-pass palindromic FAST 256-bit schedules whose tiles all fit the device at once (2^18 .. 2^20)
@@ -1511,8 +1617,11 @@ struct PlanImpl final : PlanBase {
       return NTT_ERR_HIP;
     }
     if (launch_build_tw<E>(d_full_pm, elems, r[0], tile_log_of<E>() - r[0], 0, d_tab + off_los_i,
-                           d_tab + off_hi_ipm, lo_bits, Fi, st) != hipSuccess)
+                           d_tab + off_hi_ipm, lo_bits, Fi, st) != hipSuccess) {
+      (void)hipFree(d_full_pm);  // never leave a partly built table behind as if it were built
+      d_full_pm = nullptr;
       return NTT_ERR_HIP;
+    }
     return NTT_OK;
   }
 
@@ -1599,9 +1708,9 @@ static int make_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, const 
                      unsigned log_n, int device, unsigned flags) {
   if (log_n > 40) return NTT_ERR_ARG;
   if (limbs64 != 1 && limbs64 != 4 && limbs64 != 6) return NTT_ERR_ARG;  // before packing into p32[12] / g32[12]
-  const unsigned rivals = flags & (NTT_PLAN_STOCKHAM | NTT_PLAN_GZKP | NTT_PLAN_NAIVE);
+  const unsigned rivals = flags & (NTT_PLAN_STOCKHAM | NTT_PLAN_GZKP | NTT_PLAN_NAIVE | NTT_PLAN_NO_SWAP);
   if (rivals & (rivals - 1)) return NTT_ERR_ARG;  // one rival schedule per plan
-  if ((flags & NTT_PLAN_IN_PLACE) && (flags & (NTT_PLAN_STOCKHAM | NTT_PLAN_GZKP | NTT_PLAN_NAIVE | NTT_PLAN_TWIDDLE_ONLY)))
+  if ((flags & NTT_PLAN_IN_PLACE) && (rivals || (flags & NTT_PLAN_TWIDDLE_ONLY)))
     return NTT_ERR_ARG;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return NTT_ERR_NODEV;
@@ -1667,9 +1776,25 @@ static bool wide_tiles_enabled() {
   return on;
 }
 
+// The second plan is an optimisation: when it cannot be built the plan runs alone, and nothing of the
+// failure may leak into the plan's calls.  A failed hipMalloc inside its init leaves the error as the
+// thread's last HIP error, which the next launch check (hipGetLastError) would return as NTT_ERR_HIP
+// from a healthy plan, so it is cleared here.  It is not attempted at all when the
+// device is short of memory (its scratch and tables take ~100 MiB at 2^20).  NTT_TEST_WIDE_FAIL=1
+// (tests only) makes the attempt fail through a refused allocation.
+static constexpr size_t kWideMinFreeBytes = 512ull << 20;
+// NTT_PLAN_SINGLE_LAUNCH plans (BASELINE config 2's "single-kernel" form) get the second plan too:
+// their batch-1 transforms are then ONE launch of the two passes (k_fused2b; in place k_fused2bi),
+// and the second plan is kept only if that single launch is available (single_launch_ready).  An
+// in-place single-launch plan sends only its plain forward / inverse there (wide_transforms_only).
+static bool wide_flags_ok(unsigned flags) {
+  const unsigned f = flags & ~NTT_PLAN_MONTGOMERY_IO;
+  return f == 0 || f == NTT_PLAN_SINGLE_LAUNCH || f == (NTT_PLAN_SINGLE_LAUNCH | NTT_PLAN_IN_PLACE);
+}
 static void make_wide_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, const uint64_t* g64,
                            unsigned limbs64, unsigned log_n, int device, unsigned flags) {
-  if (limbs64 != 4 || log_n != 20 || (flags & ~NTT_PLAN_MONTGOMERY_IO) != 0 || !wide_tiles_enabled()) return;
+  if (limbs64 != 4 || log_n != 20 || !wide_flags_ok(flags) || !wide_tiles_enabled()) return;
+  if ((flags & NTT_PLAN_IN_PLACE) && (flags & NTT_PLAN_MONTGOMERY_IO)) return;
   uint32_t p32[12] = {0}, g32[12] = {0};
   for (unsigned i = 0; i < 4; ++i) {
     p32[2 * i] = (uint32_t)p64[i];
@@ -1677,8 +1802,25 @@ static void make_wide_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, 
     g32[2 * i] = (uint32_t)g64[i];
     g32[2 * i + 1] = (uint32_t)(g64[i] >> 32);
   }
-  auto impl = std::make_unique<PlanImpl<Eng256T>>();
-  if (impl->init(p32, g32, log_n, device, flags) == NTT_OK) out = std::move(impl);  // else: the plan alone
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (cur != device) (void)hipSetDevice(device);
+  size_t free_b = 0, total_b = 0;
+  const bool room = hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b >= kWideMinFreeBytes;
+  if (room) {
+    const char* tf = getenv("NTT_TEST_WIDE_FAIL");
+    if (tf && tf[0] == '1') {
+      void* p = nullptr;
+      if (hipMalloc(&p, ~(size_t)0 >> 4) == hipSuccess) (void)hipFree(p);  // refused: the sticky error
+    } else {
+      auto impl = std::make_unique<PlanImpl<Eng256T>>();
+      if (impl->init(p32, g32, log_n, device, flags) == NTT_OK &&
+          (!(flags & NTT_PLAN_SINGLE_LAUNCH) || impl->single_launch_ready()))
+        out = std::move(impl);
+    }
+  }
+  if (!out) (void)hipGetLastError();  // the plan runs alone, with a clean error state
+  if (cur != device) (void)hipSetDevice(cur);
 }
 
 static int set_err(int rc) {
@@ -1692,26 +1834,37 @@ struct ntt_plan {
   std::unique_ptr<PlanBase> impl;
   std::unique_ptr<PlanBase> wide;  // one vector's transforms of a 2^20 4-limb plan (make_wide_plan)
   PlanBase* last = nullptr;        // the plan that ran the latest transform (ntt_plan_last_launch_ms)
-  // The plan that transforms `batch` vectors, remembered for the profiling readers.
-  PlanBase& exec(unsigned batch) {
-    last = (wide && batch == 1) ? wide.get() : impl.get();
+  // In-place single-launch plans: the second plan runs the plain forward / inverse only (its
+  // k_fused2bi); polymul, cosets and the fused pointwise inverse stay on the 1024-element tiles.
+  bool wide_transforms_only() const {
+    return wide && (wide->flags & NTT_PLAN_IN_PLACE) && (wide->flags & NTT_PLAN_SINGLE_LAUNCH);
+  }
+  // The plan that transforms `batch` vectors (plain forward / inverse: transform = true), remembered
+  // for the profiling readers.
+  PlanBase& exec(unsigned batch, bool transform = false) {
+    last = (wide && batch == 1 && (transform || !wide_transforms_only())) ? wide.get() : impl.get();
     return *last;
   }
 };
 
 extern "C" {
 
-int ntt_plan_create_custom_ex(ntt_plan** out, const uint64_t* modulus, const uint64_t* generator, unsigned limbs64,
-                              unsigned log_n, int device, unsigned flags) {
+static int create_plan(ntt_plan** out, const uint64_t* modulus, const uint64_t* generator, unsigned limbs64,
+                       unsigned log_n, int device, unsigned flags, bool allow_wide) {
   if (!out || !modulus || !generator) return set_err(NTT_ERR_ARG);
   *out = nullptr;
   std::unique_ptr<PlanBase> impl;
   int rc = make_plan(impl, modulus, generator, limbs64, log_n, device, flags);
   if (rc != NTT_OK) return set_err(rc);
   std::unique_ptr<PlanBase> wide;
-  make_wide_plan(wide, modulus, generator, limbs64, log_n, device, flags);
+  if (allow_wide) make_wide_plan(wide, modulus, generator, limbs64, log_n, device, flags);
   *out = new ntt_plan{std::move(impl), std::move(wide)};
   return set_err(NTT_OK);
+}
+
+int ntt_plan_create_custom_ex(ntt_plan** out, const uint64_t* modulus, const uint64_t* generator, unsigned limbs64,
+                              unsigned log_n, int device, unsigned flags) {
+  return create_plan(out, modulus, generator, limbs64, log_n, device, flags, true);
 }
 
 int ntt_plan_create_custom(ntt_plan** out, const uint64_t* modulus, const uint64_t* generator, unsigned limbs64,
@@ -1723,7 +1876,8 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
   return ntt_plan_create_ex(out, field_id, log_n, limbs64, device, 0);
 }
 
-int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags) {
+static int create_field_plan(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device,
+                             unsigned flags, bool allow_wide) {
   if (field_id < 0 || field_id > 2) return set_err(NTT_ERR_ARG);
   if (limbs64 != 1 && limbs64 != 4 && limbs64 != 6) return set_err(NTT_ERR_ARG);
   if (limbs64 == 1 && field_id != NTT_FIELD_P469762049) return set_err(NTT_ERR_ARG);
@@ -1731,7 +1885,11 @@ int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned li
   uint64_t p[6] = {0}, g[6] = {0};
   for (unsigned i = 0; i < limbs64 && i < 4; ++i) p[i] = F.p[i];
   g[0] = F.g;
-  return ntt_plan_create_custom_ex(out, p, g, limbs64, log_n, device, flags);
+  return create_plan(out, p, g, limbs64, log_n, device, flags, allow_wide);
+}
+
+int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags) {
+  return create_field_plan(out, field_id, log_n, limbs64, device, flags, true);
 }
 
 // Every entry point that launches work runs it on the plan's device (saved and restored around
@@ -1754,16 +1912,16 @@ static int on_device(ntt_plan* plan, F&& f, bool check_watchdog = true) {
 extern "C++" inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
 
 int ntt_forward(ntt_plan* plan, void* d, void* s) {
-  return on_device(plan, [&](PlanBase&) { return plan->exec(1).run(d, 1, false, S(s)); });
+  return on_device(plan, [&](PlanBase&) { return plan->exec(1, true).run(d, 1, false, S(s)); });
 }
 int ntt_inverse(ntt_plan* plan, void* d, void* s) {
-  return on_device(plan, [&](PlanBase&) { return plan->exec(1).run(d, 1, true, S(s)); });
+  return on_device(plan, [&](PlanBase&) { return plan->exec(1, true).run(d, 1, true, S(s)); });
 }
 int ntt_forward_batch(ntt_plan* plan, void* d, unsigned b, void* s) {
-  return on_device(plan, [&](PlanBase&) { return plan->exec(b).run(d, b, false, S(s)); });
+  return on_device(plan, [&](PlanBase&) { return plan->exec(b, true).run(d, b, false, S(s)); });
 }
 int ntt_inverse_batch(ntt_plan* plan, void* d, unsigned b, void* s) {
-  return on_device(plan, [&](PlanBase&) { return plan->exec(b).run(d, b, true, S(s)); });
+  return on_device(plan, [&](PlanBase&) { return plan->exec(b, true).run(d, b, true, S(s)); });
 }
 
 static int run_coset(ntt_plan* plan, void* d, const uint64_t* shift, bool inv, void* s) {
@@ -2060,6 +2218,9 @@ int plan_build_fs_table(ntt_plan* plan, void* table, unsigned log_rows, unsigned
 }
 size_t plan_table_entry_bytes(const ntt_plan* plan) { return plan && plan->impl ? plan->impl->table_entry_bytes() : 0; }
 int plan_device(const ntt_plan* plan) { return plan && plan->impl ? plan->impl->device : -1; }
+int plan_create_internal(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device) {
+  return create_field_plan(out, field_id, log_n, limbs64, device, 0, false);
+}
 unsigned plan_passes_for(const ntt_plan* plan, unsigned log_x) {
   return plan && plan->impl ? plan->impl->passes_for(log_x) : 99u;
 }

@@ -147,9 +147,9 @@ int ntt_rplan_create(ntt_rplan** out, int field_id, unsigned log_n, unsigned lim
     rp->log_n1 = log_n - rp->log_n2;
     rp->log_r = rp->log_n1 - rp->log_g;
     rp->log_c = rp->log_n2 - rp->log_g;
-    rc = ntt_plan_create(&rp->rows, field_id, rp->log_n2, limbs64, device);
+    rc = plan_create_internal(&rp->rows, field_id, rp->log_n2, limbs64, device);
   }
-  if (rc == NTT_OK) rc = ntt_plan_create(&rp->cols, field_id, rp->log_n1, limbs64, device);
+  if (rc == NTT_OK) rc = plan_create_internal(&rp->cols, field_id, rp->log_n1, limbs64, device);
   if (rc == NTT_OK) {
     uint64_t n = 0;
     unsigned eb = 0;

@@ -407,16 +407,33 @@ class DistNTT:
         self._x_windows: Optional[list] = None
         self._x_open: Optional[list] = None
 
+    @classmethod
+    def piece_candidates(cls, layout: Layout):
+        """The exchange schedules tune_pieces measures: 1 x 1, two pieces on either side of the
+        exchange and on both (2 x 1, 1 x 2, 2 x 2), and the auto_pieces size rule -- each clipped to the
+        rows / columns a rank owns, duplicates dropped.  Round 4's list was 1 x 1 plus the size rule
+        only, which at 2^24 over 8 ranks (2^21 elements per rank, below both piece minimums) left the
+        single candidate 1 x 1: the "measured choice" measured nothing.  At world
+        size 1 there is no exchange to hide: 1 x 1 only."""
+        if layout.world == 1:
+            return [(1, 1)]
+        auto = (cls.auto_pieces(layout.local_n),
+                cls.auto_pieces(layout.local_n, cap=4, min_elems=cls.MIN_COL_PIECE_ELEMS))
+        out = []
+        for p, q in [(1, 1), (2, 1), (1, 2), (2, 2), auto]:
+            c = (pow2_pieces(p, layout.r), pow2_pieces(q, layout.c))
+            if c not in out:
+                out.append(c)
+        return out
+
     def tune_pieces(self, x: torch.Tensor, candidates=None, steps: int = 8, warmup: int = 3) -> dict:
         """Plan-time measurement of the exchange schedule (FFTW_MEASURE-style; tune_four_step): every
-        rank times forward(x) with 1 x 1 and the auto_pieces rule, and the fastest becomes this plan's
+        rank times forward(x) under each of piece_candidates(), and the fastest becomes this plan's
         schedule.  Whether pieces pay depends on the link rate against the local transforms, which only
         the node at hand can say.  Collective over the group; x is overwritten."""
         L = self.layout
         if candidates is None:
-            auto = (self.auto_pieces(L.local_n),
-                    self.auto_pieces(L.local_n, cap=4, min_elems=self.MIN_COL_PIECE_ELEMS))
-            candidates = [(1, 1)] + ([auto] if auto != (1, 1) else [])
+            candidates = self.piece_candidates(L)
         dev = torch.device("cpu") if self.host_exchange else x.device
         self.fs, res = tune_four_step(L, self.engine, self, self.dist, self.group, x, candidates, steps, warmup,
                                       dev, torch.cuda.synchronize)

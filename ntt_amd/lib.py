@@ -25,6 +25,7 @@ NTT_PLAN_GZKP = 8
 NTT_PLAN_IN_PLACE = 16
 NTT_PLAN_SINGLE_LAUNCH = 32
 NTT_PLAN_NAIVE = 64
+NTT_PLAN_NO_SWAP = 128
 
 # Every symbol declared in include/ntt.h with its ctypes prototype: (restype, argtypes).
 _vp = C.c_void_p

@@ -80,7 +80,8 @@ class NTTPlan:
     def __init__(self, field_id: int = 1, log_n: int = 10, limbs64: int = 4, device: int = 0,
                  modulus: Optional[int] = None, generator: Optional[int] = None, twiddle_only: bool = False,
                  montgomery_io: bool = False, stockham: bool = False, gzkp: bool = False,
-                 in_place: bool = False, single_launch: bool = False, naive: bool = False):
+                 in_place: bool = False, single_launch: bool = False, naive: bool = False,
+                 no_swap: bool = False):
         self._lib = _L.load()
         self.log_n = int(log_n)
         self.n = 1 << self.log_n
@@ -99,6 +100,8 @@ class NTTPlan:
         flags |= _L.NTT_PLAN_GZKP if gzkp else 0
         # naive: the reference's `naive` rival (bit reversal + one radix-2 round per launch)
         flags |= _L.NTT_PLAN_NAIVE if naive else 0
+        # no_swap: the reference's `naive_no_swap` rival (radix-2 Stockham autosort, one round per launch)
+        flags |= _L.NTT_PLAN_NO_SWAP if no_swap else 0
         # in_place: no plan scratch, palindromic passes + tile-swap digit reversal (the reference's
         # self-sort-in-place property, GZKP-NTT.cu:1359-1449; ntt.h NTT_PLAN_IN_PLACE)
         flags |= _L.NTT_PLAN_IN_PLACE if in_place else 0

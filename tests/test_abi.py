@@ -133,7 +133,7 @@ def test_python_constants_match_the_header():
     text = open(os.path.join(INCLUDE, "ntt.h")).read()
     defs = {m.group(1): int(m.group(2)) for m in
             re.finditer(r"^#define\s+(NTT_(?:PLAN|ERR|FIELD)_\w+|NTT_OK)\s+\(?(-?\d+)u?\)?", text, flags=re.M)}
-    assert "NTT_PLAN_NAIVE" in defs and "NTT_ERR_DEVICE" in defs
+    assert "NTT_PLAN_NAIVE" in defs and "NTT_PLAN_NO_SWAP" in defs and "NTT_ERR_DEVICE" in defs
     for name, value in defs.items():
         assert hasattr(L, name), name
         assert getattr(L, name) == value, (name, getattr(L, name), value)
@@ -145,7 +145,7 @@ def test_conflicting_schedule_flags_are_rejected_without_a_device():
     from ntt_amd import lib as L
     so = L.load()
     h = C.c_void_p()
-    rivals = (L.NTT_PLAN_STOCKHAM, L.NTT_PLAN_GZKP, L.NTT_PLAN_NAIVE)
+    rivals = (L.NTT_PLAN_STOCKHAM, L.NTT_PLAN_GZKP, L.NTT_PLAN_NAIVE, L.NTT_PLAN_NO_SWAP)
     bad = [a | b for i, a in enumerate(rivals) for b in rivals[i + 1:]]
     bad += [r | L.NTT_PLAN_IN_PLACE for r in rivals] + [L.NTT_PLAN_IN_PLACE | L.NTT_PLAN_TWIDDLE_ONLY]
     for flags in bad:

@@ -49,3 +49,18 @@ def test_kat_check_matches_the_definition():
         bad[3] = (bad[3] + 1) % p
         assert not bench._kat_check(fid, log_n, 4, bad, ks)
         assert bench._to_ints(torch.tensor([[5, 0, 0, 0], [-1, 1, 0, 0]])) == [5, (1 << 64) - 1 + (1 << 64)]
+
+
+def test_launcher_parent_never_loads_torch():
+    """spawn_ranks (``python bench.py --gpus N`` without a launcher) counts devices in a child process:
+    the parent that later starts the ranks never imports torch, so it cannot have touched the HIP
+    runtime (here no device is visible, so it refuses after counting)."""
+    code = ("import os, sys, types; sys.path.insert(0, %r); os.environ['HIP_VISIBLE_DEVICES'] = ''\n"
+            "os.environ.pop('NTT_BENCH_EXCHANGE', None)\n"
+            "import bench\n"
+            "rc = bench.spawn_ranks(types.SimpleNamespace(gpus=2))\n"
+            "assert rc == 2, rc\n"
+            "assert 'torch' not in sys.modules, 'the launcher parent imported torch'\n"
+            "print('parent clean')\n" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "parent clean" in r.stdout, (r.stdout, r.stderr)

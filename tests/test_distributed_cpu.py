@@ -206,7 +206,25 @@ def test_piece_ranges_and_auto_pieces():
     assert DistNTT.auto_pieces(1 << 21, cap=4, min_elems=DistNTT.MIN_COL_PIECE_ELEMS) == 1
 
 
-def _tune_worker(rank, world, port, field_id, log_n, L, q):
+def test_piece_candidates_give_the_tuner_a_choice_at_every_world_size():
+    """at 2^24 over 8 ranks (2^21 elements per rank, below both auto-piece
+    minimums) round 4's candidate list was 1 x 1 alone.  Every N > 1 now measures at least 1 x 1,
+    2 x 1, 1 x 2 and 2 x 2 (clipped to the rank's rows / columns); world size 1 only 1 x 1."""
+    from ntt_amd.distributed import DistNTT, Layout
+    for log_n, log_n2 in ((24, 10), (24, 12), (28, 14), (12, 6)):
+        for world in (2, 4, 8):
+            c = DistNTT.piece_candidates(Layout(log_n, world, 0, log_n2))
+            assert len(c) >= 2 and c[0] == (1, 1) and len(set(c)) == len(c), (log_n, world, c)
+            if log_n >= 24:
+                assert {(1, 1), (2, 1), (1, 2), (2, 2)} <= set(c), (log_n, world, c)
+        assert DistNTT.piece_candidates(Layout(log_n, 1, 0, log_n2)) == [(1, 1)]
+    # 2^24 over 2 ranks: the size rule adds its 2 x 4
+    assert (2, 4) in DistNTT.piece_candidates(Layout(24, 2, 0, 10))
+    # 2^24 over 8 ranks (2^21 per rank): the four small schedules, no auto addition
+    assert DistNTT.piece_candidates(Layout(24, 8, 0, 10)) == [(1, 1), (2, 1), (1, 2), (2, 2)]
+
+
+def _tune_worker(rank, world, port, field_id, log_n, L, q, cands=None):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from ntt_amd.distributed import Layout, tune_four_step
@@ -221,7 +239,12 @@ def _tune_worker(rank, world, port, field_id, log_n, L, q):
         eng = CpuOracleEngine(field_id, log_n, L, world, rank)
         lay = Layout(log_n, world, rank)
         scratch = share.clone()
-        fs, res = tune_four_step(lay, eng, GlooPieceExchange(lay), dist, None, scratch, [(1, 1), (2, 2), (4, 1)],
+        if cands is None:
+            cands = [(1, 1), (2, 2), (4, 1)]
+        elif cands == "dist":  # the candidate list DistNTT.tune_pieces uses
+            from ntt_amd.distributed import DistNTT
+            cands = DistNTT.piece_candidates(lay)
+        fs, res = tune_four_step(lay, eng, GlooPieceExchange(lay), dist, None, scratch, cands,
                                  steps=1, warmup=0, device=torch.device("cpu"), sync=lambda: None)
         fs.forward(share)  # the chosen schedule computes the same transform
         q.put((rank, share.numpy().tobytes(), res["chosen"], sorted(res["ms_per_transform"])))
@@ -252,6 +275,35 @@ def test_tune_four_step_picks_one_schedule_on_every_rank():
     import numpy as np
     assert len({res[r][1] for r in range(world)}) == 1, res
     assert res[0][2] == ["1x1", "2x2", "4x1"]
+    shares = [torch.from_numpy(np.frombuffer(res[r][0], dtype=np.int64).copy().reshape(-1, L)) for r in range(world)]
+    X = gather_cols(shares, Layout, log_n, world, L)
+    p_, g_ = R.FIELDS[field_id]
+    assert X == R.ntt_dit(R.random_vector(field_id, 1 << log_n, seed=78), p_, g_)
+
+
+def test_tune_four_step_world8_measures_several_candidates():
+    """The N = 8 shape (world 8, gloo): the tuner times DistNTT.piece_candidates' schedules (more
+    than one), every rank picks the same one, and its forward equals the definition."""
+    from ntt_amd.distributed import Layout
+    from tests.dist_helpers import gather_cols
+    world, field_id, log_n, L = 8, 1, 8, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tune_worker, args=(r, world, port, field_id, log_n, L, q, "dist"))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rank, fwd, chosen, keys = q.get(timeout=240)
+        res[rank] = (fwd, chosen, keys)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import numpy as np
+    assert len({res[r][1] for r in range(world)}) == 1, res
+    assert len(res[0][2]) >= 2, res[0][2]
     shares = [torch.from_numpy(np.frombuffer(res[r][0], dtype=np.int64).copy().reshape(-1, L)) for r in range(world)]
     X = gather_cols(shares, Layout, log_n, world, L)
     p_, g_ = R.FIELDS[field_id]

@@ -6,7 +6,10 @@ BN254 / BLS12-381 Fr, and bit-for-bit agreement with the default four-step DIF s
 * "gzkp": GZKP(B, G) (GZKP-NTT.cu:115-233; parallel-load.cu for P): bit reversal, then in-place DIT
   passes with input twiddles (KIND_DIT, plan flag NTT_PLAN_GZKP);
 * "naive": the reference's `naive` (GZKP-NTT.cu:59-95, big-num.cu:67-170): bit reversal, then one
-  radix-2 DIT round per launch (k_naive_round, plan flag NTT_PLAN_NAIVE)."""
+  radix-2 DIT round per launch (k_naive_round, plan flag NTT_PLAN_NAIVE);
+* "no_swap": the reference's `naive_no_swap` (GZKP-NTT.cu:237-296, checked against the CPU NTT in its
+  main, :1653-1660): a radix-2 Stockham autosort, one round per launch, natural order in and out
+  (k_noswap_round, plan flag NTT_PLAN_NO_SWAP)."""
 import os
 
 import numpy as np
@@ -21,13 +24,13 @@ GOLD = np.load(os.path.join(os.path.dirname(__file__), "golden", "ref_p469762049
 THREADS = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "8"))))
 
 
-RIVALS = ["stockham", "gzkp", "naive"]
+RIVALS = ["stockham", "gzkp", "naive", "no_swap"]
 
 
 def _plan(fid, log_n, L, sched):
     from ntt_amd.ntt import NTTPlan
     return NTTPlan(field_id=fid, log_n=log_n, limbs64=L, stockham=sched == "stockham", gzkp=sched == "gzkp",
-                   naive=sched == "naive")
+                   naive=sched == "naive", no_swap=sched == "no_swap")
 
 
 @pytest.mark.parametrize("sched", RIVALS)
@@ -79,24 +82,28 @@ def test_rival_2pow24_bn254_elementwise(sched):
 def test_rival_flags_are_exclusive():
     from ntt_amd.ntt import NTTPlan
     for kw in ({"stockham": True, "gzkp": True}, {"stockham": True, "naive": True}, {"gzkp": True, "naive": True},
-               {"naive": True, "in_place": True}):
+               {"naive": True, "in_place": True}, {"no_swap": True, "naive": True}, {"no_swap": True, "in_place": True}):
         with pytest.raises(Exception):
             NTTPlan(field_id=1, log_n=12, limbs64=4, **kw)
-    with pytest.raises(Exception):  # the rivals cover P and the 4 x 64-bit layout
-        NTTPlan(field_id=2, log_n=12, limbs64=6, naive=True)
+    for kw in ({"naive": True}, {"no_swap": True}):
+        with pytest.raises(Exception):  # the rivals cover P and the 4 x 64-bit layout
+            NTTPlan(field_id=2, log_n=12, limbs64=6, **kw)
 
 
+@pytest.mark.parametrize("sched", ["naive", "no_swap"])
 @pytest.mark.parametrize("fid,L,log_n", [(0, 1, 1), (0, 1, 2), (0, 1, 5), (1, 4, 1), (1, 4, 3), (2, 4, 9)])
-def test_naive_small_sizes_vs_oracle(fid, L, log_n):
-    """The naive rival has no tile constraints: every size from 2 points, forward against the
-    oracle, the plan's (default-schedule) inverse back to the input; two launch groups recorded."""
+def test_naive_small_sizes_vs_oracle(fid, L, log_n, sched):
+    """The radix-2 rivals have no tile constraints: every size from 2 points (odd and even round
+    counts: no_swap's odd ones end in the plan buffer and are copied back), forward against the
+    oracle, the plan's (default-schedule) inverse back to the input; the launch groups recorded."""
     p, g = R.FIELDS[fid]
-    pl = _plan(fid, log_n, L, "naive")
+    pl = _plan(fid, log_n, L, sched)
     a = pl.fill(pl.empty(), "random", seed=7 + log_n)
     x = a.cpu().numpy().view(np.uint64).reshape(-1, L).copy()
     pl.set_profiling(True)
     pl.forward(a)
-    assert len(pl.last_launch_ms()) == 2  # [bit reversal, the log2 n rounds]
+    # naive: [bit reversal, the log2 n rounds]; no_swap: [the log2 n rounds]
+    assert len(pl.last_launch_ms()) == (2 if sched == "naive" else 1)
     pl.set_profiling(False)
     got = a.cpu().numpy().view(np.uint64).reshape(-1, L)
     if L == 1:

@@ -35,11 +35,13 @@ def fused_mode(request, monkeypatch):
 
 
 @pytest.mark.parametrize("kind", ["iota", "random"])
-def test_c2_2pow20_single_launch_vs_oracle(kind, fused_mode):
+def test_c2_2pow20_single_launch_vs_oracle(kind):
+    """C2 as ONE kernel (round 5): the two passes of the 4096-element tiles (10 + 10) with one grid
+    barrier, a plain launch (k_fused2b)."""
     fid, log_n = 1, 20
     p, g = R.FIELDS[fid]
     pl = _plan(fid, log_n, True)
-    assert pl.passes == [7, 7, 6]
+    assert pl.passes == [10, 10]
     t = pl.fill(pl.empty(), kind, seed=2)
     x = _host(t).copy()
     pl.set_profiling(True)
@@ -64,8 +66,8 @@ def test_c2_2pow20_single_launch_vs_oracle(kind, fused_mode):
 def test_single_launch_matches_default_schedule(fid, log_n, fused_mode):
     ref = _plan(fid, log_n, False)
     fused = _plan(fid, log_n, True)
-    # a default 2^20 plan reports its single-vector schedule, the 4096-element tiles' 10 + 10
-    assert len(fused.passes) == 3 and (ref.passes == fused.passes or (log_n, ref.passes) == (20, [10, 10]))
+    # 2^20 plans report their single-vector schedule, the 4096-element tiles' 10 + 10 (k_fused2b)
+    assert fused.passes == ref.passes and len(fused.passes) == (2 if log_n == 20 else 3)
     a = ref.fill(ref.empty(), "random", seed=log_n)
     b = a.clone()
     x = a.clone()
@@ -116,13 +118,14 @@ def _ip_plan(fid, log_n, single=True):
 
 @pytest.mark.parametrize("kind", ["iota", "random"])
 def test_c2_2pow20_in_place_single_launch_vs_oracle(kind):
-    """2^20 BN254 as ONE kernel with no scratch (k_fused3bi): passes 1 and 2 in place, the final pass's
-    digit reversal behind a third grid barrier.  Bit for bit against the threaded C oracle (forward and
-    inverse), the KAT of x_j = j, exactly one launch, and no plan buffer."""
+    """2^20 BN254 as ONE kernel with no scratch (round 5: k_fused2bi on 4096-element tiles): pass 1 in
+    place, the final pass's digit reversal behind a second grid barrier.  Bit for bit against the
+    threaded C oracle (forward and inverse), the KAT of x_j = j, exactly one launch, and no plan
+    buffer."""
     fid, log_n = 1, 20
     p, g = R.FIELDS[fid]
     pl = _ip_plan(fid, log_n)
-    assert pl.passes == [7, 6, 7]
+    assert pl.passes == [10, 10]
     t = pl.fill(pl.empty(), kind, seed=2)
     x = _host(t).copy()
     pl.set_profiling(True)
@@ -187,13 +190,18 @@ print("plain-launch ok")
 """
 
 
-def test_grid_barrier_forms_as_plain_launches():
-    """NTT_FUSED_COOP=0 (read once per process, so in a child process): the grid-barrier single
-    launches, default and in place, as plain launches give the default schedule's results."""
+@pytest.mark.parametrize("env", [{"NTT_FUSED_COOP": "0", "NTT_FUSED_MODE": "1"},
+                                 {"NTT_WIDE_TILES": "0", "NTT_FUSED_MODE": "1"},
+                                 {"NTT_WIDE_TILES": "0", "NTT_FUSED_MODE": "0"}],
+                         ids=["plain_launch", "three_pass_2pow20_barriers", "three_pass_2pow20_dataflow"])
+def test_grid_barrier_forms_in_child_processes(env):
+    """Environment switches are read once per process, so in a child process: NTT_FUSED_COOP=0, the
+    grid-barrier single launches (default and in place) as plain launches; NTT_WIDE_TILES=0, the
+    1024-element-tile single launches at 2^20 too (k_fused3b / k_fused3 / k_fused3bi, as before round
+    5).  Each gives the default schedule's results."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, NTT_FUSED_COOP="0", NTT_FUSED_MODE="1")
-    r = subprocess.run([sys.executable, "-c", _PLAIN_LAUNCH_CHECK.format(root=root)], env=env,
+    r = subprocess.run([sys.executable, "-c", _PLAIN_LAUNCH_CHECK.format(root=root)], env=dict(os.environ, **env),
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "plain-launch ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

@@ -8,7 +8,6 @@ stores, the plan's host-mapped report word is set, and the NEXT call on the plan
 NTT_ERR_DEVICE without any device query.  ntt_plan_device_status reports bit 0 and clears the
 report; with the default limit restored the plan is correct again.  The reference asserts instead
 (GZKP-NTT.cu:1527)."""
-import time
 
 import pytest
 import torch
@@ -64,8 +63,9 @@ def test_watchdog_trip_is_reported_and_plan_recovers(flag, log_n, direction, mon
 
 def test_blocking_shim_does_not_wait_for_other_streams():
     """SSIP / NTT_GZKP_256 wait on an event after their own launches (GZKP-NTT.cu:1547), not on the
-    whole device: a long queue of transforms on another (non-blocking) stream is still running when
-    the shim returns."""
+    whole device: work queued on another (non-blocking) stream is still running when the shim
+    returns.  The side stream starts with a ~2 s spin kernel, far longer than any shim call, so the
+    check needs no wall-clock bound."""
     from ntt_amd.ntt import NTTPlan, SSIP
     big = NTTPlan(1, 24, 4)
     y = _fresh(big, 5)
@@ -74,14 +74,14 @@ def test_blocking_shim_does_not_wait_for_other_streams():
     torch.cuda.synchronize()
     side = torch.cuda.Stream()
     with torch.cuda.stream(side):
+        if hasattr(torch.cuda, "_sleep"):
+            torch.cuda._sleep(int(4e9))  # ~2 s of clock cycles: the side stream is busy long after the shim
         for _ in range(300):  # ~0.45 s of transforms
             big.forward(y, stream=side)
-    t0 = time.perf_counter()
     out = SSIP(x.clone(), 3, 12)
-    dt = time.perf_counter() - t0
     still_running = not side.query()
     side.synchronize()
-    assert still_running and dt < 0.2, (still_running, dt)
+    assert still_running
     x2 = x.clone()
     SSIP(x2, 3, 12)
     assert torch.equal(out, x2)

@@ -123,12 +123,15 @@ def test_routed_calls_match_the_1024_tile_plan(tmp_path):
 
 
 def test_other_plans_keep_their_tiles():
-    """Only default (or Montgomery-I/O) 4-limb plans of exactly 2^20 take the second plan."""
+    """Only default (or Montgomery-I/O, or single-launch) 4-limb plans of exactly 2^20 take the second
+    plan."""
     from ntt_amd.ntt import NTTPlan
     assert NTTPlan(1, 19, 4).passes == [7, 6, 6]
     assert NTTPlan(1, 21, 4).passes == [7, 7, 7]
     assert len(NTTPlan(1, 20, 4, in_place=True).passes) == 3
-    assert len(NTTPlan(1, 20, 4, single_launch=True).passes) == 3
+    # round 5: single-launch plans of 2^20 run the two passes as one launch (k_fused2b / k_fused2bi)
+    assert NTTPlan(1, 20, 4, single_launch=True).passes == [10, 10]
+    assert NTTPlan(1, 20, 4, single_launch=True, in_place=True).passes == [10, 10]
     assert len(NTTPlan(2, 20, 6).passes) == 3
 
 
@@ -148,3 +151,37 @@ def test_custom_modulus_plan_and_256_bit_shim_take_the_two_pass_plan():
     assert torch.equal(a, b) and torch.equal(a, c)
     custom.inverse(b)
     assert torch.equal(b, x)
+
+
+_CHILD_FAIL = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, {root!r})
+from ntt_amd.ntt import NTTPlan
+pl = NTTPlan(1, 20, 4)  # the second plan's init is refused (NTT_TEST_WIDE_FAIL=1)
+assert pl.passes == [7, 7, 6], pl.passes
+x = pl.fill(pl.empty(), "random", seed=51)
+t = x.clone()
+pl.forward(t)  # the first call on the plan: must not see the refused allocation's error
+y = t.clone()
+pl.inverse(y)
+assert torch.equal(y, x)
+np.save({path!r}, t.cpu().numpy())
+print("child ok")
+"""
+
+
+def test_failed_second_plan_leaves_no_error_behind(tmp_path):
+    """when the 4096-element-tile plan cannot be built (its allocation refused),
+    the plan runs alone on 1024-element tiles and its first forward returns NTT_OK with the same
+    output as a plan that has the second plan (the refused allocation's sticky error is cleared)."""
+    from ntt_amd.ntt import NTTPlan
+    path = str(tmp_path / "fail.npy")
+    env = dict(os.environ, NTT_TEST_WIDE_FAIL="1")
+    r = subprocess.run([sys.executable, "-c", _CHILD_FAIL.format(root=ROOT, path=path)], env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "child ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+    pl = NTTPlan(1, 20, 4)
+    assert pl.passes == [10, 10]
+    t = pl.fill(pl.empty(), "random", seed=51)
+    pl.forward(t)
+    assert np.array_equal(t.cpu().numpy(), np.load(path))

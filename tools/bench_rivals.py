@@ -34,8 +34,9 @@ def main():
     from ntt_amd.ntt import NTTPlan
     rows = []
     for fid, L, lg in ((1, 4, 24), (1, 4, 20), (0, 1, 24), (0, 1, 26)):
-        for sched in ("default", "stockham", "gzkp", "naive"):
-            pl = NTTPlan(fid, lg, L, stockham=(sched == "stockham"), gzkp=(sched == "gzkp"), naive=(sched == "naive"))
+        for sched in ("default", "stockham", "gzkp", "naive", "no_swap"):
+            pl = NTTPlan(fid, lg, L, stockham=(sched == "stockham"), gzkp=(sched == "gzkp"), naive=(sched == "naive"),
+                         no_swap=(sched == "no_swap"))
             t = pl.fill(pl.empty(), "random", seed=1)
             pl.set_profiling(True)
             s = timeit(lambda: pl.forward(t))

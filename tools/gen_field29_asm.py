@@ -91,6 +91,87 @@ def gen_mont():
     return "\n".join(o)
 
 
+# ---------------------------------------------------------------- paired columns
+# The column form above is ONE dependent v_mad_u64_u32 chain per product: 93 % of the MADs of the
+# radix-256 column pass read the accumulator the previous instruction wrote (tools/isa_chains.py),
+# and products run back to back, so a wave's MADs never overlap.  Here two adjacent columns K and
+# K + 1 share one asm statement as two chains whose MADs alternate: column K + 1 starts from 0
+# instead of from column K's carry, and the carry is added after both (one 64-bit add per column
+# pair).  The sums are the same values as the single chain's (same bounds), with 2 more VGPRs.
+def stmt2(pa, pb, indent="  "):
+    """one statement: chain A (acc, carried in) and chain B (accb, from 0) with alternating MADs."""
+    lines, ops = [], []
+    k = 4
+    ia = ib = 0
+    first_b = True
+    while ia < len(pa) or ib < len(pb):
+        for which in ("a", "b"):
+            if which == "a" and ia < len(pa):
+                a, b, bs = pa[ia]
+                ia += 1
+                lines.append(f"v_mad_u64_u32 %0, %2, %{k}, %{k + 1}, %0")
+            elif which == "b" and ib < len(pb):
+                a, b, bs = pb[ib]
+                ib += 1
+                lines.append(f"v_mad_u64_u32 %1, %3, %{k}, %{k + 1}, {'0' if first_b else '%1'}")
+                first_b = False
+            else:
+                continue
+            ops.append(f'"v"({a})')
+            ops.append(f'"{"s" if bs else "v"}"({b})')
+            k += 2
+    body = "\\n\\t".join(lines)
+    out = [f'{indent}asm("{body}"', f'{indent}    : "+v"(acc), "=&v"(accb), "=&s"(cc), "=&s"(cc2)']
+    oplines = [", ".join(ops[i:i + 6]) for i in range(0, len(ops), 6)]
+    out.append(f"{indent}    : " + (",\n" + indent + "      ").join(oplines) + ");")
+    return "\n".join(out)
+
+
+def gen_mulc_pair(uniform=False):
+    o = []
+    name = "mulc29_a9u" if uniform else "mulc29_a9"
+    o.append(f"__device__ __forceinline__ void {name}(uint32_t (&r)[9], const uint32_t (&x)[9], const uint32_t (&w)[9],")
+    o.append("                                          const uint32_t (&ws)[9], const uint32_t (&pbar)[9]) {")
+    o.append("  uint32_t q[9];")
+    o.append("  uint64_t acc = 0, accb, cc, cc2;")
+    o.append("  // q = floor(x * ws / B) from columns >= 7 (see mulc29), columns in pairs (7, 8) ... (15, 16)")
+    cols = list(range(L - 2, 2 * L - 1))
+    hi_terms = lambda K: [(f"x[{i}]", f"ws[{K - i}]", uniform) for i in range(max(0, K - (L - 1)), min(K, L - 1) + 1)]
+    for a in range(0, len(cols), 2):
+        K = cols[a]
+        if a + 1 < len(cols):
+            o.append(stmt2(hi_terms(K), hi_terms(K + 1)))
+            if K >= L:
+                o.append(f"  q[{K - L}] = (uint32_t)acc & kMask29;")
+            o.append("  accb += acc >> 29;")
+            if K + 1 >= L:
+                o.append(f"  q[{K + 1 - L}] = (uint32_t)accb & kMask29;")
+            o.append("  acc = accb >> 29;")
+        else:
+            o.append(stmt(hi_terms(K)))
+            if K >= L:
+                o.append(f"  q[{K - L}] = (uint32_t)acc & kMask29;")
+            o.append("  acc >>= 29;")
+    o.append("  q[8] = (uint32_t)acc;")
+    o.append("  acc = 0;")
+    o.append("  // r = (x * w + q * pbar) mod B, columns in pairs (0, 1) ... (6, 7), then 8")
+    lo_terms = lambda K: ([(f"x[{i}]", f"w[{K - i}]", uniform) for i in range(K + 1)] +
+                          [(f"q[{i}]", f"pbar[{K - i}]", True) for i in range(K + 1)])
+    for K in range(0, L, 2):
+        if K + 1 < L:
+            o.append(stmt2(lo_terms(K), lo_terms(K + 1)))
+            o.append(f"  r[{K}] = (uint32_t)acc & kMask29;")
+            o.append("  accb += acc >> 29;")
+            o.append(f"  r[{K + 1}] = (uint32_t)accb & kMask29;")
+            if K + 2 < L:
+                o.append("  acc = accb >> 29;")
+        else:
+            o.append(stmt(lo_terms(K)))
+            o.append(f"  r[{K}] = (uint32_t)acc & kMask29;")
+    o.append("}")
+    return "\n".join(o)
+
+
 # ---------------------------------------------------------------- one asm statement per product
 # The column form above still pays hipcc's fixed boundary pad (an s_nop after every ;;#ASMEND whose
 # outputs a VALU reads next): ~17 per product.  Here the whole product, shifts and masks included, is
@@ -189,6 +270,9 @@ def main():
     print("#ifndef NTT_ASM_WHOLE")
     print("#define NTT_ASM_WHOLE 0  // measured slower: 1.73 vs 1.67 ms (2^24 BN254; spills, no ILP across products)")
     print("#endif")
+    print("#ifndef NTT_MULC_PAIR")
+    print("#define NTT_MULC_PAIR 0")
+    print("#endif")
     print("#if defined(__HIP_DEVICE_COMPILE__) && NTT_ASM_WHOLE")
     print("// one asm statement per product (see the generator)")
     print(gen_mulc_whole())
@@ -198,6 +282,13 @@ def main():
     print("                                           const uint32_t (&ws)[9], const uint32_t (&pbar)[9]) {")
     print("  mulc29_a9(r, x, w, ws, pbar);")
     print("}")
+    print("#elif defined(__HIP_DEVICE_COMPILE__) && NTT_MULC_PAIR")
+    print("// two product columns per asm statement, their MAD chains interleaved (see the generator)")
+    print(gen_mulc_pair())
+    print()
+    print(gen_mulc_pair(uniform=True))
+    print()
+    print(gen_mont())
     print("#elif defined(__HIP_DEVICE_COMPILE__)")
     print("// one asm statement per product column")
     print(gen_mulc())

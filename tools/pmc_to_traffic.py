@@ -7,7 +7,9 @@ fetch and write passes and matched by dispatch order.  Writes profiles/pmc_summa
     {tag: {"launch_bytes": [bytes of launch 0, launch 1, ...], "src_hash": H, "profile": DIR}}
 where H = ntt_amd.build.source_hash() of the tree that was profiled (bench.py reports the bytes only
 while the kernel sources still hash to H).
-Usage: python tools/pmc_to_traffic.py gpurun_out/pmc TAG [profiles/pmc_summary.json]
+Usage: python tools/pmc_to_traffic.py gpurun_out/pmc TAG [profiles/pmc_summary.json] [--per K] [--note TEXT]
+--per K: K launches per step (the four-step's rank-local rows + columns, tools/pmc_ranklocal.sh),
+instead of the tail heuristic; --note: stored with the entry (what the bytes cover).
 """
 import csv
 import glob
@@ -31,8 +33,18 @@ def per_dispatch(root, counter):
 
 
 def main():
-    root, tag = sys.argv[1], sys.argv[2]
-    out = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_summary.json"
+    argv = list(sys.argv[1:])
+    per_arg, note = None, None
+    if "--per" in argv:
+        i = argv.index("--per")
+        per_arg = int(argv[i + 1])
+        del argv[i:i + 2]
+    if "--note" in argv:
+        i = argv.index("--note")
+        note = argv[i + 1]
+        del argv[i:i + 2]
+    root, tag = argv[0], argv[1]
+    out = argv[2] if len(argv) > 2 else "profiles/pmc_summary.json"
     fetch = [(k, v) for k, v in per_dispatch(os.path.join(root, "fetch"), "FETCH_SIZE") if "k_pass" in k]
     write = [(k, v) for k, v in per_dispatch(os.path.join(root, "write"), "WRITE_SIZE") if "k_pass" in k]
     # launches per transform = number of distinct consecutive pass kernels at the tail
@@ -40,6 +52,8 @@ def main():
     per = 1
     while per < len(names) and not ("KIND_FINAL" in names[per - 1] or ", 1, " in names[per - 1]):
         per += 1
+    if per_arg:
+        per = per_arg
     steps = len(fetch) // per
     traffic = []
     for i in range(per):
@@ -50,6 +64,8 @@ def main():
     from ntt_amd.build import source_hash
     d = json.load(open(out)) if os.path.exists(out) else {}
     d[tag] = {"launch_bytes": traffic, "src_hash": source_hash(), "profile": root}
+    if note:
+        d[tag]["note"] = note
     json.dump(d, open(out, "w"), indent=1)
     print(tag, [f"{t / 1e9:.3f} GB" for t in traffic])
 
