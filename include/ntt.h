@@ -105,17 +105,21 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
  * 8192-element tiles) and the rival schedules return NTT_ERR_ARG. */
 #define NTT_PLAN_IN_PLACE 16u
 /* Single-launch schedule (BASELINE config 2, "single-kernel self-sort-in-place"; the reference runs
- * 2^20 as 4 launches, GZKP-NTT.cu:1509-1545): a 3-pass forward / inverse of a 4-limb BN254 / BLS12-381
- * plan (2^18 .. 2^24) runs as ONE persistent launch: two grid-wide barriers in a cooperative launch
- * (k_fused3b; the default) or the passes' tiles handed between workgroups through dependency
- * counters (k_fused3; environment NTT_FUSED_MODE=0), instead of kernel boundaries.  With
- * NTT_PLAN_IN_PLACE too (2^18 .. 2^20): no scratch, three grid barriers (k_fused3bi).  Same contract
- * and results as the default schedule; batch 1; other plans and calls ignore the flag.
- * The cooperative launch costs ~20 us per call (it guarantees that every workgroup is resident at
- * once).  Environment NTT_FUSED_COOP=0 launches the grid-barrier forms as plain launches, after the
- * plan has checked that the grid fits the device: 2^18 then ties three launches, 2^20 comes within
- * ~4 %.  Only for a process that never runs two single-launch plans at once: two such kernels on
- * different streams can each hold part of the device and wait for the other, until the watchdog.
+ * 2^20 as 4 launches, GZKP-NTT.cu:1509-1545): a forward / inverse of a 4-limb BN254 / BLS12-381 plan
+ * runs as ONE persistent launch.  At 2^20 (round 5): the two passes of 4096-element tiles (10 + 10)
+ * with one grid barrier (k_fused2b); with NTT_PLAN_IN_PLACE too, no scratch and a second barrier
+ * before the digit-reversed stores (k_fused2bi).  Other 3-pass sizes (2^18 .. 2^24): two grid-wide
+ * barriers (k_fused3b; the default) or the passes' tiles handed between workgroups through dependency
+ * counters (k_fused3; environment NTT_FUSED_MODE=0); in place (2^18, 2^19): three barriers
+ * (k_fused3bi).  Same contract and results as the default schedule; batch 1; other plans and calls
+ * ignore the flag.
+ * The grid-barrier forms are plain launches of at most as many workgroups as the device keeps
+ * resident (the plan's occupancy query), so they assume no other persistent kernel holds part of the
+ * device meanwhile: two single-launch plans on two streams of one device could each wait for the
+ * other's workgroups.  Every wait is bounded: such a call returns garbage and the plan's next call
+ * NTT_ERR_DEVICE (ntt_plan_device_status), never a hang.  Environment NTT_FUSED_COOP=1 uses a
+ * cooperative launch instead (co-residency guaranteed, ~20 us more per call; under rocprofv3 such
+ * processes crashed at exit in round 4).
  * ntt_plan_device_status reports a wait that gave up (a watchdog; never expected). */
 #define NTT_PLAN_SINGLE_LAUNCH 32u
 /* Rival schedule, the reference's `naive` (GZKP-NTT.cu:59-95, big-num.cu:67-170): the bit reversal,

@@ -31,5 +31,7 @@ int plan_device(const ntt_plan* plan);
 int plan_create_internal(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device);
 // pass kernels that a 2^log_x-point transform takes with this plan's engine (the four-step split)
 unsigned plan_passes_for(const ntt_plan* plan, unsigned log_x);
+// the largest pass radix (log2) of that transform's schedule
+unsigned plan_max_radix_for(const ntt_plan* plan, unsigned log_x);
 
 }  // namespace ntt

@@ -1233,11 +1233,16 @@ hipError_t launch_fused3(int r1, int r2, int r3, const uint32_t* src, uint32_t* 
     const dim3 g(F.nwg), b((1 << E::TILE_LOG) / E::EPT);
     FusedKArgs<E> K{src, scratch, dst, A1, A2, A3, F};
     void* kargs[] = {&K};
-    static const bool coop = [] {  // NTT_FUSED_COOP=0: a plain launch of the grid-barrier forms (A/B)
+    // Round 5: the grid-barrier forms are PLAIN launches by default, after the plan's occupancy check
+    // that the grid fits the device (fused3_capacity).  hipLaunchCooperativeKernel cost ~20 us per call
+    // (DESIGN §4), and every rocprofv3-traced process that made one crashed in the runtime's exit
+    // handlers ("exit-time SIGSEGV").  NTT_FUSED_COOP=1: the cooperative launch (which
+    // guarantees co-residency even beside other persistent kernels).
+    static const bool coop = [] {
       const char* v = getenv("NTT_FUSED_COOP");
-      return !(v && *v == '0');
+      return v && *v == '1';
     }();
-    // mode 1: a cooperative launch (every workgroup resident, or the launch fails: never a hang)
+    // mode 1: with NTT_FUSED_COOP=1 a cooperative launch (every workgroup resident, or the launch fails)
     if (F.mode == 2) {  // in place: cooperative launch of exactly one workgroup per tile
 #define NTT_FUSED_IP_CASE(a, c, d)                                                                \
   if (r1 == a && r2 == c && r3 == d) {                                                            \
@@ -1935,9 +1940,9 @@ template <class E, int LOGR, int KIND, bool FULLTW, bool FAST, int FSM>
 static hipError_t launch_plain(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, dim3 g, dim3 b,
                                hipStream_t st) {
   if constexpr (KIND == KIND_COLUMN && FULLTW && FAST && E::SHOUP_OUTER) {
-    if (A.tw_sh) {  // later column passes: Shoup-pair outer twiddles (they read scratch)
-      if (A.src_user) return hipErrorInvalidValue;
+    if (A.tw_sh) {  // Shoup-pair outer twiddles: later column passes, or pass 1 of a small plan
       constexpr bool SU = E::SCRW == E::MEMW;  // one instance when scratch and caller layouts agree
+      if (A.src_user && !SU) return hipErrorInvalidValue;
       hipLaunchKernelGGL((k_pass<E, LOGR, KIND, true, true, PRO_NONE, SU, FSM, true>), g, b, 0, st, src, dst, A);
       return hipGetLastError();
     }

@@ -128,8 +128,10 @@ struct PlanBase {
   virtual int build_fs_table(void* table, unsigned log_rows, unsigned log_cols, uint64_t row0, uint64_t col0,
                              bool inverse, hipStream_t st) = 0;
   virtual size_t table_entry_bytes() const = 0;
-  // pass kernels a transform of 2^log_x points takes with this plan's engine (its schedule())
+  // pass kernels a transform of 2^log_x points takes with this plan's engine (its schedule()), and
+  // the largest radix (log2) among them
   virtual unsigned passes_for(unsigned log_x) const = 0;
+  virtual unsigned max_radix_for(unsigned log_x) const = 0;
   virtual int coset(void* d, const uint64_t* shift, unsigned limbs64, bool inverse, hipStream_t st) = 0;
   virtual int count_noncanonical(const void* d, uint64_t count, uint64_t* bad, hipStream_t st) = 0;
   virtual int device_status(unsigned* bad) = 0;
@@ -880,41 +882,57 @@ struct PlanImpl final : PlanBase {
     return NTT_OK;
   }
 
-  // Column passes 2..p-1 whose table is small enough to stay in L2 (N_i entries of E::TW words <=
-  // 8 MiB): Shoup pairs instead of w R_e, so their outer-twiddle product is a Shoup product (143
-  // MADs) instead of a Montgomery one (162).  Measured (profiles/r02_sh/): 2^24 pass 2 (5 MiB table)
+  // Column passes whose table is small enough to stay in L2 (N_i entries of E::TW words <= 8 MiB):
+  // Shoup pairs instead of w R_e, so their outer-twiddle product is a Shoup product (143 MADs)
+  // instead of a Montgomery one (162).  Measured (profiles/r02_sh/): 2^24 pass 2 (5 MiB table)
   // -0.5 %, 2^28 pass 3 (1.3 MiB) -1.2 %, 2^28 pass 2 (168 MiB, not L2-resident) +6 % -- hence the cap.
-  // NTT_SHOUP_OUTER=0 in the environment keeps the Montgomery tables (A/B switch).
+  // Round 5: pass 1 too when its table fits (plans of <= 2^16 points: the four-step's 2^16-point
+  // column transforms of 2^24, C4's 2^14-point rows and columns), on engines whose scratch and caller
+  // layouts agree (one kernel instance reads both); the inverse's pass-1 table carries n^-1 as its
+  // Montgomery twin does.  NTT_SHOUP_OUTER=0 in the environment keeps the Montgomery tables (A/B
+  // switch); =1 keeps pass 1 on its Montgomery table (round-4 behaviour).
+  static int shoup_outer_env() {
+    static const int v = [] {
+      const char* e = getenv("NTT_SHOUP_OUTER");
+      return e && *e ? atoi(e) : 2;
+    }();
+    return v;
+  }
   int build_shoup_tables() {
     if constexpr (!E::SHOUP_OUTER) {
       return NTT_OK;
     } else {
-      if (const char* v = getenv("NTT_SHOUP_OUTER"); v && v[0] == '0') return NTT_OK;
-      if (npass < 3 || !Ff.red_ok) return NTT_OK;  // the Shoup-pair column kernels are FAST instances
+      if (shoup_outer_env() == 0) return NTT_OK;
+      if (npass < 2 || !Ff.red_ok) return NTT_OK;  // the Shoup-pair column kernels are FAST instances
       constexpr size_t kMaxTableBytes = 8ull << 20;
+      constexpr bool pass1_ok = E::SCRW == E::MEMW;  // pass 1 reads the caller's layout
+      const unsigned i0 = (pass1_ok && shoup_outer_env() >= 2) ? 0u : 1u;
       size_t elems = 0;
-      unsigned blk = log_n - r[0];
-      for (unsigned i = 1; i + 1 < npass; ++i) {
+      unsigned blk = log_n;
+      for (unsigned i = 0; i + 1 < npass; ++i) {
         full_sh_off[0][i] = elems;
-        full_sh_ok[i] = ((1ull << blk) * TW * 4) <= kMaxTableBytes;
+        full_sh_ok[i] = i >= i0 && ((1ull << blk) * TW * 4) <= kMaxTableBytes;
         if (full_sh_ok[i]) elems += 1ull << blk;
         blk -= r[i];
       }
       if (elems == 0) return NTT_OK;
       size_t free_b = 0, total_b = 0;
       if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return NTT_OK;
-      if (2 * elems * TW * 4 > free_b / 8) return NTT_OK;
+      if (2 * elems * TW * 4 > free_b / 8) {
+        for (auto& ok : full_sh_ok) ok = false;
+        return NTT_OK;
+      }
       if (hipMalloc(&d_full_sh, 2 * elems * TW * 4) != hipSuccess) return NTT_ERR_HIP;
       for (int dir = 0; dir < 2; ++dir) {
-        blk = log_n - r[0];
-        for (unsigned i = 1; i + 1 < npass; ++i) {
+        blk = log_n;
+        for (unsigned i = 0; i + 1 < npass; ++i) {
           full_sh_off[dir][i] = dir * elems + full_sh_off[0][i];
           if (!full_sh_ok[i]) {
             blk -= r[i];
             continue;
           }
           const uint32_t* lo = d_tab + (dir ? off_los_i : off_los_f);
-          const uint32_t* hi = d_tab + (dir ? off_hi_i : off_hi_f);
+          const uint32_t* hi = d_tab + (dir ? (i == 0 ? off_hi_is : off_hi_i) : off_hi_f);
           if (launch_build_tw_sh<E>(d_full_sh + full_sh_off[dir][i] * TW, 1ull << blk, r[i], tile_log_of<E>() - r[i],
                                     log_n - blk, lo, hi, lo_bits, dir ? Fi : Ff, d_tab + off_pinvB,
                                     nullptr) != hipSuccess)
@@ -1090,6 +1108,13 @@ struct PlanImpl final : PlanBase {
       return 99;
     return p == 0 ? 1 : p;
   }
+  unsigned max_radix_for(unsigned log_x) const override {
+    unsigned rr[8] = {0}, p = 0;
+    if (!schedule(log_x, tile_log_of<E>(), E::MIN_COLS_LOG, E::NARROW_FIRST, rr, p)) return 99;
+    unsigned m = p == 0 ? log_x : 0;
+    for (unsigned i = 0; i < p; ++i) m = rr[i] > m ? rr[i] : m;
+    return m;
+  }
 
   int run(void* d, unsigned batch, bool inverse, hipStream_t st) override {
     if (!d || batch == 0 || (flags & NTT_PLAN_TWIDDLE_ONLY)) return NTT_ERR_ARG;
@@ -1174,17 +1199,19 @@ struct PlanImpl final : PlanBase {
         }();
         A.tw_full = (full_dir && (i > 0 || E::PASS1_FULL_TABLE || p1_full)) ? d_fulls[inverse ? 1 : 0] + full_off[i] * TABW
                                                                              : nullptr;
-        if (i > 0 && d_full_sh && full_sh_ok[i]) {
+        if (d_full_sh && full_sh_ok[i] && (i > 0 || full_dir)) {
           A.tw_full = d_full_sh + full_sh_off[inverse ? 1 : 0][i] * TW;
           A.tw_sh = 1;
         }
-        if (i == 0 && in2) {
+        if (i == 0 && in2) {  // the fused prologues bring their own pass-1 tables (w R_e)
           A.src2 = in2;
           A.tw_full = d_full_pm;
+          A.tw_sh = 0;
         }
         if (i == 0 && tw_in) {
           A.tw_in = tw_in;
           A.tw_full = full0;
+          A.tw_sh = 0;
         }
         A.log_blk = blk + il;
         A.log_m = log_n - blk;
@@ -2220,6 +2247,9 @@ size_t plan_table_entry_bytes(const ntt_plan* plan) { return plan && plan->impl 
 int plan_device(const ntt_plan* plan) { return plan && plan->impl ? plan->impl->device : -1; }
 int plan_create_internal(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device) {
   return create_field_plan(out, field_id, log_n, limbs64, device, 0, false);
+}
+unsigned plan_max_radix_for(const ntt_plan* plan, unsigned log_x) {
+  return plan && plan->impl ? plan->impl->max_radix_for(log_x) : 99u;
 }
 unsigned plan_passes_for(const ntt_plan* plan, unsigned log_x) {
   return plan && plan->impl ? plan->impl->passes_for(log_x) : 99u;

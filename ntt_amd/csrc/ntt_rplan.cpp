@@ -74,20 +74,28 @@ FsMap map1(unsigned lc, uint64_t ps) { return FsMap{lc, lc, ps, 0}; }
 FsMap map2(unsigned lc, uint64_t ps, unsigned lc2, uint64_t ps2) { return FsMap{lc, lc2, ps, ps2}; }
 
 // The split n = n1 n2 (log_n2 returned): fewest pass kernels over the row (length n2) and column
-// (length n1) transforms, the most balanced split among equals.  2^24 on the 256-bit engines: 12 + 12
-// takes 2 + 2 passes, 14 + 10 takes 2 + 1 (the rows one workgroup tile each) -- as many HBM passes
-// as the one-GPU transform; 2^28 stays 14 + 14 (4 passes either way).
+// (length n1) transforms, then the smallest largest radix among those passes, then the most balanced
+// split.  2^24 on the 256-bit engines: 12 + 12 takes 2 + 2 passes; 14 + 10, 15 + 9 and 16 + 8 take
+// 2 + 1 (the rows one workgroup tile each), as many HBM passes as the one-GPU transform, and 16 + 8 has
+// the smallest radices (8 + 8 column passes, radix-256 rows): its rank-local launches measured 1.06 /
+// 1.07 / 1.13 x (1/G of the one-GPU transform) at G = 2 / 4 / 8, against 1.09 / 1.12 / 1.16 x for
+// 14 + 10 (round 5, profiles/r05_ranklocal/).  14 + 10 runs 5.25 products per element in its radix-1024
+// row launch where 16 + 8 runs 4.06 (the one-GPU transform's count).  2^28 stays 14 + 14 (4 passes of
+// radix 2^7).
 unsigned choose_split(const ntt_plan* tw, unsigned log_n, unsigned log_g) {
   const unsigned bal = log_n / 2;
   if (const char* e = std::getenv("NTT_FS_LOG_N2")) {  // experiments (tools/ab_env.sh): a fixed n2
     const unsigned v = (unsigned)std::atoi(e);
     if (v >= 3 && v >= log_g && v <= bal) return v;
   }
-  unsigned best = bal, best_p = ~0u;
+  unsigned best = bal, best_p = ~0u, best_r = ~0u;
   for (unsigned s2 = bal; s2 >= 3 && s2 >= log_g; --s2) {
     const unsigned p = plan_passes_for(tw, log_n - s2) + plan_passes_for(tw, s2);
-    if (p < best_p) {
+    const unsigned r1 = plan_max_radix_for(tw, log_n - s2), r2 = plan_max_radix_for(tw, s2);
+    const unsigned r = r1 > r2 ? r1 : r2;
+    if (p < best_p || (p == best_p && r < best_r)) {
       best_p = p;
+      best_r = r;
       best = s2;
     }
   }

@@ -90,11 +90,12 @@ def test_piece_entry_points_reject_bad_pieces():
 
 
 def test_rank_plan_split_takes_fewest_passes():
-    """ntt_rplan_create's split: balanced unless a narrower n2 saves a pass kernel (2^24 BN254:
-    14 + 10 = 2 + 1 passes instead of 12 + 12 = 2 + 2; 2^20 keeps 10 + 10; C4's 2^28 keeps 14 + 14,
-    asserted in test_gpu_fullsize)."""
+    """ntt_rplan_create's split: fewest pass kernels, then the smallest largest radix, then the most
+    balanced (round 5).  2^24 BN254: 16 + 8 (2 + 1 passes of radix <= 2^8; 12 + 12 takes 2 + 2, 14 + 10
+    has a radix-2^10 row pass); 2^22: 14 + 8; 2^20 keeps 10 + 10 (1 + 1); C4's 2^28 keeps 14 + 14,
+    asserted in test_gpu_fullsize."""
     from ntt_amd.distributed import RankPlan
-    for log_n, world, n2 in ((24, 1, 10), (24, 8, 10), (22, 2, 10), (20, 4, 10), (16, 2, 8)):
+    for log_n, world, n2 in ((24, 1, 8), (24, 8, 8), (22, 2, 8), (20, 4, 10), (16, 2, 8)):
         rp = RankPlan(1, log_n, 4, world, 0, 0)
         assert (rp.layout.log_n1, rp.layout.log_n2) == (log_n - n2, n2), log_n
         del rp

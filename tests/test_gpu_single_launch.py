@@ -190,13 +190,14 @@ print("plain-launch ok")
 """
 
 
-@pytest.mark.parametrize("env", [{"NTT_FUSED_COOP": "0", "NTT_FUSED_MODE": "1"},
+@pytest.mark.parametrize("env", [{"NTT_FUSED_COOP": "1", "NTT_FUSED_MODE": "1"},
                                  {"NTT_WIDE_TILES": "0", "NTT_FUSED_MODE": "1"},
                                  {"NTT_WIDE_TILES": "0", "NTT_FUSED_MODE": "0"}],
-                         ids=["plain_launch", "three_pass_2pow20_barriers", "three_pass_2pow20_dataflow"])
+                         ids=["cooperative_launch", "three_pass_2pow20_barriers", "three_pass_2pow20_dataflow"])
 def test_grid_barrier_forms_in_child_processes(env):
-    """Environment switches are read once per process, so in a child process: NTT_FUSED_COOP=0, the
-    grid-barrier single launches (default and in place) as plain launches; NTT_WIDE_TILES=0, the
+    """Environment switches are read once per process, so in a child process: NTT_FUSED_COOP=1, the
+    grid-barrier single launches (default and in place) as cooperative launches (round 5: plain
+    launches are the default); NTT_WIDE_TILES=0, the
     1024-element-tile single launches at 2^20 too (k_fused3b / k_fused3 / k_fused3bi, as before round
     5).  Each gives the default schedule's results."""
     import subprocess

@@ -70,9 +70,25 @@ def main():
     t = pl.fill(pl.empty(), "random", seed=2)
     emit("C2: 2^20 forward BN254 Fr as ONE kernel (NTT_PLAN_SINGLE_LAUNCH)", 1 << 20,
          timeit(lambda: pl.forward(t), steps=50), passes=pl.passes,
-         note="bit-exact with the 3-launch line above; slower, so a plan flag (DESIGN.md §4)")
+         note="round 5: the two passes of 4096-element tiles with one grid barrier, a plain launch (k_fused2b); "
+              "bit-exact with the default line above (DESIGN.md §4)")
     assert pl.device_status() == 0
     del pl, t
+    # ... in place: BASELINE C2's "single-kernel self-sort-in-place" (no scratch, k_fused2bi)
+    pl = NTTPlan(1, 20, 4, single_launch=True, in_place=True)
+    t = pl.fill(pl.empty(), "random", seed=2)
+    emit("C2: 2^20 forward BN254 Fr as ONE kernel in place (NTT_PLAN_SINGLE_LAUNCH | NTT_PLAN_IN_PLACE)", 1 << 20,
+         timeit(lambda: pl.forward(t), steps=50), passes=pl.passes)
+    assert pl.device_status() == 0
+    del pl, t
+    # a 3-pass single launch (grid barriers, plain launch since round 5): 2^22
+    for sl in (False, True):
+        pl = NTTPlan(1, 22, 4, single_launch=sl)
+        t = pl.fill(pl.empty(), "random", seed=2)
+        emit(f"2^22 forward BN254 Fr{' as ONE kernel (k_fused3b)' if sl else ''}", 1 << 22,
+             timeit(lambda: pl.forward(t), steps=50), passes=pl.passes)
+        assert pl.device_status() == 0
+        del pl, t
 
     # C3
     for L in (4, 6):

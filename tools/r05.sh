@@ -38,6 +38,19 @@ for s in $ARGS; do
     rl) step ranklocal_fwd 300 python3 -u tools/exp_ranklocal.py --out $O/ranklocal_fwd.jsonl
         step ranklocal_inv 300 python3 -u tools/exp_ranklocal.py --inverse --out $O/ranklocal_inv.jsonl ;;
     rl_split) for v in 8 9; do step ranklocal_n2_$v 300 env NTT_FS_LOG_N2=$v python3 -u tools/exp_ranklocal.py --out $O/ranklocal_n2_$v.jsonl; done ;;
+    rl_ab) # the split rule's A/B on one box: default (16 + 8 since round 5) against 14 + 10, forward and inverse, twice
+      for i in 1 2; do
+        step rl_default_fwd_$i 300 python3 -u tools/exp_ranklocal.py --out $O/rl_default_fwd_$i.jsonl
+        step rl_n2_10_fwd_$i 300 env NTT_FS_LOG_N2=10 python3 -u tools/exp_ranklocal.py --out $O/rl_n2_10_fwd_$i.jsonl
+      done
+      step rl_default_inv 300 python3 -u tools/exp_ranklocal.py --inverse --out $O/rl_default_inv.jsonl
+      step rl_n2_10_inv 300 env NTT_FS_LOG_N2=10 python3 -u tools/exp_ranklocal.py --inverse --out $O/rl_n2_10_inv.jsonl ;;
+    rl_sh) # pass-1 Shoup tables of the 2^16 column transforms: default against NTT_SHOUP_OUTER=1, twice
+      for i in 1 2; do
+        step rl_sh_default_$i 300 python3 -u tools/exp_ranklocal.py --out $O/rl_sh_default_$i.jsonl
+        step rl_sh_off_$i 300 env NTT_SHOUP_OUTER=1 python3 -u tools/exp_ranklocal.py --out $O/rl_sh_off_$i.jsonl
+      done ;;
+    prof_configs) step rocprof_configs 900 rocprofv3 --kernel-trace --stats -d $O/prof_configs -o run --output-format csv -- python3 tools/bench_configs.py --out $O/configs_traced.jsonl ;;
     pmc_rl) step pmc_ranklocal 900 env O=$O/pmc_rl bash tools/pmc_ranklocal.sh ;;
     rivals) step rivals 600 python3 -u tools/bench_rivals.py --out $O/rivals.jsonl ;;
     prof) step rocprof_stats 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py ;;
@@ -46,6 +59,11 @@ for s in $ARGS; do
       step pmc_sq 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d $O/pmc/sq -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity --prewarm-s 0
       step pmc_fetch 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/pmc/fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity --prewarm-s 0
       step pmc_write 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc/write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-parity --prewarm-s 0 ;;
+    # the exit-time SIGSEGV of cooperative launches under rocprofv3: the probe
+    # dumps /proc/self/maps at Python exit; tools/symbolize_trace.py resolves the trace.  probe_coop is
+    # expected to crash at exit: run it LAST in a call.
+    probe_plain) step probe_plain 200 rocprofv3 --kernel-trace --stats -d $O/probe_plain -o run --output-format csv -- python3 tools/exit_crash_probe.py $O/maps_plain.txt --coop 0 ;;
+    probe_coop) step probe_coop 200 rocprofv3 --kernel-trace --stats -d $O/probe_coop -o run --output-format csv -- python3 tools/exit_crash_probe.py $O/maps_coop.txt --coop 1 ;;
     *) echo "unknown step $s" >&2; exit 2 ;;
   esac
 done
