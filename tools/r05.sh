@@ -26,6 +26,9 @@ for s in $ARGS; do
     tests) step pytest_gpu 1100 $PYT tests -m gpu ;;
     smoke) step smoke 120 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 300 python3 -u bench.py ;;
+    reh2) step bench_n2_rehearsal 400 env NTT_BENCH_EXCHANGE=host python3 -u bench.py --gpus 2 --steps 20 --warmup 10 ;;
+    reh4) step bench_n4_rehearsal 600 env NTT_BENCH_EXCHANGE=host python3 -u bench.py --gpus 4 --steps 10 --warmup 5 ;;
+    reh8) step bench_n8_rehearsal 600 env NTT_BENCH_EXCHANGE=host python3 -u bench.py --gpus 8 --steps 10 --warmup 5 ;;
     benchd) step bench_driver 300 python3 -u bench.py --steps 20 --warmup 5 ;;
     fs1) step bench_fourstep_w1 300 python3 -u bench.py --four-step --steps 20 --warmup 10 --no-cpu-baseline ;;
     c2) # the C2 forms, two interleaved repetitions, fresh process each (ms per transform over 200 calls)
