@@ -14,16 +14,18 @@ struct FsIO {
   uint32_t il = 0;                  // Mode I: log2 of the interleave
   FsMap min{}, mout{}, mepi{};      // input, output and epilogue-index maps (PassArgs)
   const void* tw_epi = nullptr;     // final-pass twiddle table (plan_build_fs_table) or null
+  bool no_scale = false;            // inverse of a single-pass plan: no n^-1 product (the caller folded
+                                    // it into another table, plan_build_fs_table's scale_log)
 };
 
 // Transform(s) of `plan` from `in` (+ `in2`: first pass starts from in * in2, polymul inverse) to
 // `out` with the four-step maps.  Mode I: 2^io.il interleaved transforms (batch ignored).
 int plan_run_fs(ntt_plan* plan, const void* in, const void* in2, void* out, unsigned batch, bool inverse,
                 const FsIO& io, hipStream_t st);
-// table[a][b] = w_n^(+-(row0 + a)(col0 + b)) in the plan's epilogue format (n = the plan's size);
-// 2^(log_rows + log_cols) entries of plan_table_entry_bytes() bytes.
+// table[a][b] = w_n^(+-(row0 + a)(col0 + b)) 2^-scale_log in the plan's epilogue format (n = the plan's
+// size); 2^(log_rows + log_cols) entries of plan_table_entry_bytes() bytes.
 int plan_build_fs_table(ntt_plan* plan, void* table, unsigned log_rows, unsigned log_cols, uint64_t row0,
-                        uint64_t col0, bool inverse, hipStream_t st);
+                        uint64_t col0, bool inverse, hipStream_t st, unsigned scale_log = 0);
 size_t plan_table_entry_bytes(const ntt_plan* plan);
 int plan_device(const ntt_plan* plan);
 // A plan for the library's own callers (the rank plan's row / column transforms, which run only

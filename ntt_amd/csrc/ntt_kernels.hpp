@@ -223,10 +223,11 @@ hipError_t launch_naive_round(const uint32_t* src, uint32_t* dst, uint32_t log_n
 template <class E>
 hipError_t launch_bitrev(const uint32_t* src, uint32_t* dst, uint32_t log_n, const uint32_t* digits, uint32_t nd,
                          hipStream_t st);
+// scale (E::TW words, a twiddle) or null: every entry is also multiplied by it
 template <class E>
 hipError_t launch_build_fs_tw(uint32_t* out, uint32_t log_rows, uint32_t log_cols, uint64_t row0, uint64_t col0,
                               uint32_t log_n, const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits,
-                              const typename E::Args& F, hipStream_t st);
+                              const typename E::Args& F, hipStream_t st, const uint32_t* scale = nullptr);
 template <class E>
 hipError_t launch_naive(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t batch, hipStream_t st);
 // Fill local element i with the synthetic value of global index

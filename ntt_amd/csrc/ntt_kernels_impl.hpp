@@ -1585,7 +1585,8 @@ hipError_t launch_bitrev(const uint32_t* src, uint32_t* dst, uint32_t log_n, con
 template <class E>
 __global__ void k_build_fs_tw(uint32_t* __restrict__ out, uint32_t log_rows, uint32_t log_cols, uint64_t row0,
                               uint64_t col0, uint32_t log_n, const uint32_t* __restrict__ lo,
-                              const uint32_t* __restrict__ hi, uint32_t lo_bits, const typename E::Args F) {
+                              const uint32_t* __restrict__ hi, uint32_t lo_bits, const typename E::Args F,
+                              const uint32_t* __restrict__ scale) {
   NTT_GRID_STRIDE(idx, (size_t(1) << (log_rows + log_cols))) {
     const uint64_t a = idx >> log_cols, b = idx & ((1ull << log_cols) - 1);
     const uint64_t e = ((row0 + a) * (col0 + b)) & ((1ull << log_n) - 1);
@@ -1593,6 +1594,10 @@ __global__ void k_build_fs_tw(uint32_t* __restrict__ out, uint32_t log_rows, uin
     E::tload(x, lo, (uint32_t)(e & ((1ull << lo_bits) - 1)));
     E::tload(y, hi, (uint32_t)(e >> lo_bits));
     E::mul(x.w, y, F);
+    if (scale) {  // a constant folded into every entry (the four-step's row n2^-1); mul takes any x < B
+      E::tload(y, scale, 0);
+      E::mul(x.w, y, F);
+    }
     E::template store<E::MUL_OUT, false, E::TABW>(out, idx, x.w, F);
   }
 }
@@ -1600,10 +1605,10 @@ __global__ void k_build_fs_tw(uint32_t* __restrict__ out, uint32_t log_rows, uin
 template <class E>
 hipError_t launch_build_fs_tw(uint32_t* out, uint32_t log_rows, uint32_t log_cols, uint64_t row0, uint64_t col0,
                               uint32_t log_n, const uint32_t* lo, const uint32_t* hi, uint32_t lo_bits,
-                              const typename E::Args& F, hipStream_t st) {
+                              const typename E::Args& F, hipStream_t st, const uint32_t* scale) {
   const size_t count = 1ull << (log_rows + log_cols);
   hipLaunchKernelGGL((k_build_fs_tw<E>), dim3(grid_1d(count)), dim3(256), 0, st, out, log_rows,
-                     log_cols, row0, col0, log_n, lo, hi, lo_bits, F);
+                     log_cols, row0, col0, log_n, lo, hi, lo_bits, F, scale);
   return hipGetLastError();
 }
 
@@ -2129,7 +2134,7 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
                                             hipStream_t);                                                         \
   template hipError_t launch_build_fs_tw<E>(uint32_t*, uint32_t, uint32_t, uint64_t, uint64_t, uint32_t,           \
                                             const uint32_t*, const uint32_t*, uint32_t, const typename E::Args&,    \
-                                            hipStream_t);                                                           \
+                                            hipStream_t, const uint32_t*);                                                           \
   template hipError_t launch_scale_pow<E>(uint32_t*, uint32_t, uint32_t, const uint32_t*, const uint32_t*, uint32_t, \
                                           const typename E::Args&, hipStream_t);                                   \
   template hipError_t launch_count_noncanonical<E>(const uint32_t*, size_t, const ModWords<E::MEMW>&,              \

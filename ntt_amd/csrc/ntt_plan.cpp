@@ -126,7 +126,7 @@ struct PlanBase {
   virtual int run_fs(const void* in, const void* in2, void* out, unsigned batch, bool inverse, const ntt::FsIO& io,
                      hipStream_t st) = 0;
   virtual int build_fs_table(void* table, unsigned log_rows, unsigned log_cols, uint64_t row0, uint64_t col0,
-                             bool inverse, hipStream_t st) = 0;
+                             bool inverse, unsigned scale_log, hipStream_t st) = 0;
   virtual size_t table_entry_bytes() const = 0;
   // pass kernels a transform of 2^log_x points takes with this plan's engine (its schedule()), and
   // the largest radix (log2) among them
@@ -450,6 +450,7 @@ struct PlanImpl final : PlanBase {
   size_t off_lo_f = 0, off_hi_f = 0, off_lo_i = 0, off_hi_i = 0, off_hi_is = 0, off_r2 = 0;
   size_t off_los_f = 0, off_los_i = 0;  // lo tables scaled by R_e (left factor of on-the-fly twiddles)
   size_t off_rm = 0;                    // R_e R^-1 (Montgomery-form pointwise product)
+  size_t off_pow2inv = 0;               // 2^-k, k = 0..log_n, E::TW words each (build_fs_table's scale)
   size_t off_hi_ipm = 0;                // inverse hi table scaled by n^-1 R_e (fused polymul, pass 1)
   uint32_t* d_full_pm = nullptr;        // inverse pass-1 outer twiddles x n^-1 R_e (fused polymul)
   uint32_t* d_stk_tab = nullptr;        // NTT_PLAN_STOCKHAM: per-pass input-twiddle tables
@@ -646,6 +647,20 @@ struct PlanImpl final : PlanBase {
       off_rm = host.size();
       EH.encode(H.from_mont(H.mul(H.to_mont(engine_radix_mod_p()), H.to_mont(rio_inv))), enc);
       host.insert(host.end(), enc, enc + TW);
+      while (host.size() % 4) host.push_back(0);
+    }
+    {  // 2^-k mod p for k = 0..log_n as twiddles (Tw encoding): the four-step folds a row transform's
+       // n2^-1 into its inverse epilogue table (build_fs_table's scale_log, ntt_rplan.cpp)
+      off_pow2inv = host.size();
+      uint32_t enc[TW];
+      std::vector<std::vector<uint32_t>> ent(log_n + 1);
+      Vec<NH> x = ninv_m;  // 2^-log_n (Montgomery form); doubling walks k down to 0
+      for (int k = (int)log_n; k >= 0; --k) {
+        EH.encode(H.from_mont(x), enc);
+        ent[k].assign(enc, enc + TW);
+        x = H.add(x, x);
+      }
+      for (unsigned k = 0; k <= log_n; ++k) host.insert(host.end(), ent[k].begin(), ent[k].end());
       while (host.size() % 4) host.push_back(0);
     }
     if constexpr (E::SHOUP_OUTER) {
@@ -1162,7 +1177,7 @@ struct PlanImpl final : PlanBase {
     } else if (npass == 1) {
       PassArgs<E> A = base_args(inverse);
       A.tw_int = d_tab + off_int[0];
-      A.flags = inverse ? 1u : 0u;
+      A.flags = (inverse && !(io && io->no_scale)) ? 1u : 0u;  // no_scale: n^-1 folded in by the caller
       set_fs(A, FS_MAP_IN | FS_MAP_OUT);
       if (io) A.tw_epi = static_cast<const uint32_t*>(io->tw_epi);
       set_extents(A, io, il);
@@ -1613,13 +1628,16 @@ struct PlanImpl final : PlanBase {
   uint32_t* d_pw = nullptr;  // gathered pointwise products of mapped pieces (run_fs), on first use
   size_t pw_elems = 0;
 
+  // scale_log k > 0: every entry also carries 2^-k (the four-step's row n2^-1, folded into the inverse
+  // columns' epilogue so that the single-pass inverse rows need no scaling product)
   int build_fs_table(void* table, unsigned log_rows, unsigned log_cols, uint64_t row0, uint64_t col0, bool inverse,
-                     hipStream_t st) override {
-    if (!table || log_rows + log_cols > 40) return NTT_ERR_ARG;
+                     unsigned scale_log, hipStream_t st) override {
+    if (!table || log_rows + log_cols > 40 || scale_log > log_n) return NTT_ERR_ARG;
     const uint32_t* lo = d_tab + (inverse ? off_los_i : off_los_f);
     const uint32_t* hi = d_tab + (inverse ? off_hi_i : off_hi_f);
+    const uint32_t* scale = scale_log ? d_tab + off_pow2inv + (size_t)scale_log * TW : nullptr;
     return launch_build_fs_tw<E>(static_cast<uint32_t*>(table), log_rows, log_cols, row0, col0, log_n, lo, hi,
-                                 lo_bits, inverse ? Fi : Ff, st) == hipSuccess
+                                 lo_bits, inverse ? Fi : Ff, st, scale) == hipSuccess
                ? NTT_OK
                : NTT_ERR_HIP;
   }
@@ -2239,9 +2257,9 @@ int plan_run_fs(ntt_plan* plan, const void* in, const void* in2, void* out, unsi
   return plan->impl->run_fs(in, in2, out, batch, inverse, io, st);
 }
 int plan_build_fs_table(ntt_plan* plan, void* table, unsigned log_rows, unsigned log_cols, uint64_t row0,
-                        uint64_t col0, bool inverse, hipStream_t st) {
+                        uint64_t col0, bool inverse, hipStream_t st, unsigned scale_log) {
   if (!plan || !plan->impl) return NTT_ERR_ARG;
-  return plan->impl->build_fs_table(table, log_rows, log_cols, row0, col0, inverse, st);
+  return plan->impl->build_fs_table(table, log_rows, log_cols, row0, col0, inverse, scale_log, st);
 }
 size_t plan_table_entry_bytes(const ntt_plan* plan) { return plan && plan->impl ? plan->impl->table_entry_bytes() : 0; }
 int plan_device(const ntt_plan* plan) { return plan && plan->impl ? plan->impl->device : -1; }

@@ -35,7 +35,10 @@ struct ntt_rplan {
   size_t elem_bytes = 0;
   ntt_plan *rows = nullptr, *cols = nullptr, *tw = nullptr;
   void* tab_fwd = nullptr;  // [r][n2]: w_n^((g r + a) k2)
-  void* tab_inv = nullptr;  // [n1][c]: w_n^-(j1 (g c + kc))
+  void* tab_inv = nullptr;  // [n1][c]: w_n^-(j1 (g c + kc)) (times n2^-1 when rows_no_scale)
+  // the row transforms are single-pass: their inverse's n2^-1 is folded into tab_inv (the inverse
+  // columns' epilogue), so the inverse rows run without their scaling product
+  bool rows_no_scale = false;
   ~ntt_rplan() {
     int cur = 0;
     (void)hipGetDevice(&cur);
@@ -170,9 +173,11 @@ int ntt_rplan_create(ntt_rplan** out, int field_id, unsigned log_n, unsigned lim
   }
   if (rc == NTT_OK) {
     const uint64_t g = (uint64_t)rank;
+    rp->rows_no_scale = plan_passes_for(rp->tw, rp->log_n2) == 1;
     rc = plan_build_fs_table(rp->tw, rp->tab_fwd, rp->log_r, rp->log_n2, g << rp->log_r, 0, false, nullptr);
     if (rc == NTT_OK)
-      rc = plan_build_fs_table(rp->tw, rp->tab_inv, rp->log_n1, rp->log_c, 0, g << rp->log_c, true, nullptr);
+      rc = plan_build_fs_table(rp->tw, rp->tab_inv, rp->log_n1, rp->log_c, 0, g << rp->log_c, true, nullptr,
+                               rp->rows_no_scale ? rp->log_n2 : 0u);
     if (rc == NTT_OK && hipDeviceSynchronize() != hipSuccess) rc = NTT_ERR_HIP;
   }
   if (rc != NTT_OK) {
@@ -256,6 +261,7 @@ int ntt_rplan_inverse_rows_range(ntt_rplan* rp, const void* d_recv, void* d_out,
   FsIO io;
   io.fs = FS_MAP_IN;
   io.min = map1(rp->log_c, rp->chunk());
+  io.no_scale = rp->rows_no_scale;
   const void* src = static_cast<const char*>(d_recv) + (row0 << rp->log_c) * rp->elem_bytes;
   void* dst = static_cast<char*>(d_out) + (row0 << rp->log_n2) * rp->elem_bytes;
   return plan_run_fs(rp->rows, src, nullptr, dst, (unsigned)nrows, true, io, S(s));
@@ -343,6 +349,7 @@ int ntt_rplan_inverse_rows_piece(ntt_rplan* rp, const void* d_recv, void* d_out,
     FsIO io;
     io.fs = FS_MAP_IN;
     io.min = map2(rp->log_c, rp->chunk(), lcm, (1ull << rp->log_r) * cm);
+    io.no_scale = rp->rows_no_scale;
     const void* src = static_cast<const char*>(d_recv) + row0 * cm * rp->elem_bytes;
     void* dst = static_cast<char*>(d_out) + (row0 << rp->log_n2) * rp->elem_bytes;
     if (int rc = plan_run_fs(rp->rows, src, nullptr, dst, (unsigned)m, true, io, S(s))) return rc;
