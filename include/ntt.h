@@ -337,8 +337,8 @@ int ntt_rplan_destroy(ntt_rplan* rp);
  * `devices`).  d_data[g] / hip_streams[g] belong to devices[g] (streams may be NULL = default
  * streams); each d_data[g] holds n / ngpus elements.  Device g runs ntt_rplan rank g.  Layouts (as
  * ntt_amd/distributed.py), with n = n1 n2, r = n1/ngpus, c = n2/ngpus, where the plan picks the split
- * (ntt_mplan_info / ntt_rplan_info): the balanced n1 = 2^ceil(log_n/2), n2 = 2^floor(log_n/2) unless
- * a narrower n2 takes fewer pass kernels (2^24 on the 256-bit engines: n1 = 2^14, n2 = 2^10):
+ * (ntt_mplan_info / ntt_rplan_info): the fewest pass kernels, then the smallest largest radix, then
+ * the most balanced split (2^24 on the 256-bit engines: n1 = 2^16, n2 = 2^8):
  *   forward input  (row layout):    d_data[g] = [r][n2], element (a, j2) = x[g r + a + n1 j2]
  *   forward output (column layout): d_data[g] = [n1][c], element (k1, kc) = X[g c + kc + n2 k1]
  * The inverse takes the column layout back to the row layout (1/n included).  Asynchronous. */

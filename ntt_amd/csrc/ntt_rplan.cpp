@@ -1,8 +1,8 @@
 // One rank of the distributed four-step NTT: the local steps around the all-to-all,
 // fused so that no separate twiddle, pack or transpose pass touches HBM.
 //
-//   n = n1 n2 with n1 >= n2: the balanced split n1 = 2^ceil(L/2), n2 = 2^floor(L/2) unless a narrower
-//   n2 needs fewer pass kernels in total (choose_split; ntt_rplan_info reports it); rank g of G owns
+//   n = n1 n2 with n1 >= n2: the fewest pass kernels in total, then the smallest largest radix, then the
+//   most balanced split (choose_split; ntt_rplan_info reports it); rank g of G owns
 //   r = n1/G rows and c = n2/G columns.  Layouts (ntt.h):
 //     row layout     [r][n2]: local (a, j2)  = x[g r + a + n1 j2]
 //     column layout  [n1][c]: local (k1, kc) = X[g c + kc + n2 k1]   (transform index fastest)

@@ -37,8 +37,8 @@ import torch
 @dataclass
 class Layout:
     """n = n1 n2 over ``world`` ranks.  ``log_n2`` None: the balanced split (n2 = 2^floor(L/2)); the
-    rank plans pick their own (ntt_rplan_info: balanced unless a narrower n2 takes fewer passes) and
-    pass it here."""
+    rank plans pick their own (ntt_rplan_info: fewest passes, then the smallest largest radix, then the
+    most balanced; 2^24 on the 256-bit engines: 16 + 8) and pass it here."""
     log_n: int
     world: int
     rank: int
