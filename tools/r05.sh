@@ -40,6 +40,7 @@ for s in $ARGS; do
     prof_coop) step rocprof_coop 200 env NTT_WIDE_TILES=0 rocprofv3 --kernel-trace --stats -d $O/prof_coop -o run --output-format csv -- python3 tools/exp_launches.py --cfg f1_L4_n20_sl --warmup 5 --steps 20 ;;
     rl) step ranklocal_fwd 300 python3 -u tools/exp_ranklocal.py --out $O/ranklocal_fwd.jsonl
         step ranklocal_inv 300 python3 -u tools/exp_ranklocal.py --inverse --out $O/ranklocal_inv.jsonl ;;
+    rl28) step ranklocal_c4 300 python3 -u tools/exp_ranklocal.py --log-n 28 --worlds 8 --warmup 5 --steps 10 --out $O/ranklocal_c4.jsonl ;;
     rl_split) for v in 8 9; do step ranklocal_n2_$v 300 env NTT_FS_LOG_N2=$v python3 -u tools/exp_ranklocal.py --out $O/ranklocal_n2_$v.jsonl; done ;;
     rl_ab) # the split rule's A/B on one box: default (16 + 8 since round 5) against 14 + 10, forward and inverse, twice
       for i in 1 2; do
