@@ -1,0 +1,5 @@
+// Eng256: k_pass instantiations for KIND_ROWS (several single-tile transforms per workgroup).
+#include "ntt_kernels_impl.hpp"
+namespace ntt {
+NTT_INSTANTIATE_KIND(Eng256, KIND_ROWS)
+}  // namespace ntt

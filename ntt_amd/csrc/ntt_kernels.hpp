@@ -12,12 +12,22 @@ namespace ntt {
 // permutation (ntt_plan_create_ex flag NTT_PLAN_STOCKHAM).
 // KIND_DIT: the GZKP(B, G) rival (GZKP-NTT.cu:115-165): in-place DIT column passes with input-side
 // twiddles w_N^(c d) over bit-reversed data (ntt_plan_create_ex flag NTT_PLAN_GZKP).
-enum : int { KIND_COLUMN = 0, KIND_FINAL = 1, KIND_SINGLE = 2, KIND_STOCKHAM = 3, KIND_DIT = 4 };
+// KIND_ROWS: a batch of short single-tile transforms (n <= 2^7), TILE / n of them per 4-wave workgroup
+// (the final pass's block layout), instead of one per workgroup (KIND_SINGLE, below one wave for
+// these n): batched short transforms and the four-step's row transforms (ntt_rplan) of such n.  At
+// n = 2^8 / 2^9 one transform per one- / two-wave workgroup is as fast or faster.
+enum : int { KIND_COLUMN = 0, KIND_FINAL = 1, KIND_SINGLE = 2, KIND_STOCKHAM = 3, KIND_DIT = 4, KIND_ROWS = 5 };
 // engines with KIND_STOCKHAM instances (ntt_e256_stk.hip, ntt_ep_stk.hip)
 template <class E>
 struct HasStockham {
   static constexpr bool value = false;
 };
+// engines with KIND_ROWS instances (ntt_e256_rows.hip) and the radices they cover
+template <class E>
+struct HasRows {
+  static constexpr bool value = false;
+};
+constexpr int kRowsMinLog = 3, kRowsMaxLog = 7;
 
 // Elements per workgroup tile of the multi-pass kernels (engines.hpp: E::TILE_LOG, E::EPT per thread).
 template <class E>
@@ -40,6 +50,10 @@ struct HasStockham<Eng256> {
 };
 template <>
 struct HasStockham<EngP> {
+  static constexpr bool value = true;
+};
+template <>
+struct HasRows<Eng256> {
   static constexpr bool value = true;
 };
 

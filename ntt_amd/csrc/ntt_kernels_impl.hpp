@@ -405,7 +405,7 @@ __device__ __forceinline__ bool ipn_grid_barrier(const PassArgs<E>& A) {
 // where it measured slower (profiles/r02_ldstw/)
 template <class E, int LOGR, int KIND>
 __host__ __device__ constexpr int pass_tile_te() {
-  return (KIND == KIND_SINGLE) ? (1 << LOGR) : (1 << tile_log_of<E>());
+  return (KIND == KIND_SINGLE) ? (1 << LOGR) : (1 << tile_log_of<E>());  // KIND_ROWS: TILE / 2^LOGR transforms
 }
 template <class E, int LOGR, int KIND>
 __host__ __device__ constexpr int pass_lds_words() {
@@ -435,6 +435,7 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
   constexpr int QB = ept_log<E>(), EPT = E::EPT;
   using S = Sched<LOGR, QB>;
   constexpr bool COLLIKE = KIND == KIND_COLUMN || KIND == KIND_STOCKHAM || KIND == KIND_DIT;  // column groups
+  constexpr bool ROWS = KIND == KIND_ROWS;  // T whole transforms per workgroup: transform w T + c
   constexpr int TE = pass_tile_te<E, LOGR, KIND>();
   constexpr int T = TE >> LOGR;  // columns (column pass) or blocks (final / single) per workgroup
   // reduce_top form (engines.hpp): radix-256 column passes are at the VGPR cap and keep the 64-bit one
@@ -463,31 +464,36 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
   // Four-step addressing (PassArgs::fs, ntt_rplan_*): the first pass may read and the last pass may
   // write through the per-peer chunk maps, and Mode I runs 2^il interleaved transforms.  All flags
   // are kernel arguments (wave-uniform branches); fs == 0 is the plain batched transform.
-  constexpr bool IN_USER = (KIND == KIND_COLUMN && SRC_USER) || KIND == KIND_SINGLE;
+  constexpr bool IN_USER = (KIND == KIND_COLUMN && SRC_USER) || KIND == KIND_SINGLE || ROWS;
   constexpr bool EPI = FSM == 2 && KIND != KIND_COLUMN;
   const bool fs_il = FSM > 0 && (A.fs & FS_IL) != 0;
   const bool map_in = FSM > 0 && IN_USER && (A.fs & FS_MAP_IN);
   const bool map_out = FSM > 0 && KIND != KIND_COLUMN && (A.fs & FS_MAP_OUT);
-  const bool single_il = KIND == KIND_SINGLE && fs_il;  // one interleaved transform per workgroup
-  const size_t bidx = (size_t)bq * (A.batch_stride / E::MEMW);  // first element of this transform
+  // one interleaved transform per workgroup (KIND_ROWS: T adjacent ones, runs of T elements)
+  const bool single_il = (KIND == KIND_SINGLE || ROWS) && fs_il;
+  const size_t tstride = A.batch_stride / E::MEMW;  // elements between batched transforms
+  const size_t bidx = (size_t)bq * tstride;         // first element of this transform (KIND_ROWS: bq = 0)
   if (!map_in && !single_il) src += bidx * SW;
   if (!map_out && !single_il) dst += bidx * DW;
   const size_t boff = bidx * E::MEMW;  // caller-buffer words (src2)
-  // input element `pos` (transform-relative; Mode I column passes: the interleaved linear index)
-  auto in_pos = [&](size_t pos) -> size_t {
-    if (single_il) pos = (pos << A.il) + bq;
+  // input element `pos` of transform b (= bq, or w T + c in KIND_ROWS; Mode I column passes: the
+  // interleaved linear index)
+  auto in_pos = [&](size_t pos, size_t b) -> size_t {
+    if (single_il) pos = (pos << A.il) + b;
+    else if (ROWS && !map_in) pos += b * tstride;
     if (!map_in) return pos;
-    return A.min(pos, fs_il ? 0 : bq);
+    return A.min(pos, fs_il ? 0 : b);
   };
   // output element (pre-map position as above) -> address; epilogue-table index of the same element
-  auto out_pos = [&](size_t pos) -> size_t {
-    if (single_il) pos = (pos << A.il) + bq;
+  auto out_pos = [&](size_t pos, size_t b) -> size_t {
+    if (single_il) pos = (pos << A.il) + b;
+    else if (ROWS && !map_out) pos += b * tstride;
     if (!map_out) return pos;
-    return A.mout(pos, fs_il ? 0 : bq);
+    return A.mout(pos, fs_il ? 0 : b);
   };
-  auto epi_idx = [&](size_t pos) -> size_t {
-    if (!fs_il) return ((size_t)bq << A.log_n) + pos;
-    if (single_il) pos = (pos << A.il) + bq;
+  auto epi_idx = [&](size_t pos, size_t b) -> size_t {
+    if (!fs_il) return (b << A.log_n) + pos;
+    if (single_il) pos = (pos << A.il) + b;
     return (A.fs & FS_MAP_EPI) ? A.mepi(pos, 0) : pos;
   };
   // debug builds: an index outside its buffer is recorded and redirected to element 0
@@ -583,12 +589,13 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
         } else {
           pos = pi;
         }
-        E::template load<SW>(x[j * Q + d], src, ck(NTT_NOMEM(IN_USER ? in_pos(pos) : pos), A.dbg_src_n));
+        const size_t b = ROWS ? (size_t)w * T + c : (size_t)bq;  // this element's transform
+        E::template load<SW>(x[j * Q + d], src, ck(NTT_NOMEM(IN_USER ? in_pos(pos, b) : pos), A.dbg_src_n));
 #if NTT_DEBUG_CHECKS
         // the caller's elements must be canonical (the reference's BAD LIMB trap); a column pass reads
         // them only when A.src_user (one SRC_USER instance also serves later passes when the scratch
         // and caller layouts agree)
-        if (KIND == KIND_SINGLE || (KIND == KIND_COLUMN && A.src_user))
+        if (KIND == KIND_SINGLE || ROWS || (KIND == KIND_COLUMN && A.src_user))
           if (!E::dbg_canonical(x[j * Q + d], A.F)) ntt_dbg_flag(A.F.dbg, NTT_DBG_INPUT);
 #endif
         if constexpr ((KIND == KIND_STOCKHAM || KIND == KIND_DIT) && FULLTW) {
@@ -603,7 +610,7 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
         }
         if constexpr (PRO == PRO_PW) {
           uint32_t y[E::W];
-          E::load(y, A.src2 + boff, in_pos(pos));  // src2 has src's layout (a four-step piece: mapped)
+          E::load(y, A.src2 + boff, in_pos(pos, b));  // src2 has src's layout (a four-step piece: mapped)
           E::mulv(x[j * Q + d], y, A.F);  // canonical inputs: < 3p, normalised
         } else if constexpr (PRO == PRO_COSET) {
           typename E::Tw u;
@@ -724,25 +731,26 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
           }
           if constexpr (EPI) {  // four-step twiddle w_n^(j1 k2) of this output (ntt_rplan), then the pack map
             uint32_t tw[E::W];
-            E::template load<E::TABW>(tw, A.tw_epi, epi_idx(pos));
+            E::template load<E::TABW>(tw, A.tw_epi, epi_idx(pos, bq));
             E::mulv(v, tw, A.F);
-            E::template store<E::MUL_OUT, FAST, DW>(dst, ck(NTT_NOMEM(out_pos(pos)), A.dbg_dst_n), v, A.F);
+            E::template store<E::MUL_OUT, FAST, DW>(dst, ck(NTT_NOMEM(out_pos(pos, bq)), A.dbg_dst_n), v, A.F);
           } else {
-            E::template store<E::IN * Q, FAST, DW>(dst, ck(NTT_NOMEM(out_pos(pos)), A.dbg_dst_n), v, A.F);
+            E::template store<E::IN * Q, FAST, DW>(dst, ck(NTT_NOMEM(out_pos(pos, bq)), A.dbg_dst_n), v, A.F);
           }
-        } else {
+        } else {  // KIND_SINGLE, KIND_ROWS
           pos = kn;
+          const size_t b = ROWS ? (size_t)w * T + c : (size_t)bq;
           if constexpr (EPI) {
             if (A.flags & 1u) E::mul(v, A.F.ninv, A.F);
             uint32_t tw[E::W];
-            E::template load<E::TABW>(tw, A.tw_epi, epi_idx(pos));
+            E::template load<E::TABW>(tw, A.tw_epi, epi_idx(pos, b));
             E::mulv(v, tw, A.F);
-            E::template store<E::MUL_OUT, FAST>(dst, ck(out_pos(pos), A.dbg_dst_n), v, A.F);
+            E::template store<E::MUL_OUT, FAST>(dst, ck(out_pos(pos, b), A.dbg_dst_n), v, A.F);
           } else if (A.flags & 1u) {
             E::mul(v, A.F.ninv, A.F);
-            E::template store<E::MUL_OUT, FAST>(dst, ck(out_pos(pos), A.dbg_dst_n), v, A.F);
+            E::template store<E::MUL_OUT, FAST>(dst, ck(out_pos(pos, b), A.dbg_dst_n), v, A.F);
           } else {
-            E::template store<E::IN * Q, FAST>(dst, ck(out_pos(pos), A.dbg_dst_n), v, A.F);
+            E::template store<E::IN * Q, FAST>(dst, ck(out_pos(pos, b), A.dbg_dst_n), v, A.F);
           }
         }
       });
@@ -1983,8 +1991,11 @@ template <class E, int KIND, int LOGR>
 static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, uint32_t grid,
                                 uint32_t batch, hipStream_t st) {
   constexpr int TL = tile_log_of<E>();
-  constexpr int MAXR = (KIND == KIND_SINGLE) ? TL : TL - E::MIN_COLS_LOG;
-  if constexpr (LOGR > MAXR || ((KIND == KIND_STOCKHAM || KIND == KIND_DIT) && !HasStockham<E>::value)) {
+  constexpr int MAXR = (KIND == KIND_SINGLE || KIND == KIND_ROWS) ? TL : TL - E::MIN_COLS_LOG;
+  // KIND_ROWS: the engines and radices ntt_e256_rows.hip instantiates (>= 2 transforms per tile), FAST only
+  constexpr bool ROWS_OFF = KIND == KIND_ROWS && (!HasRows<E>::value || !E::FASTRED || LOGR < kRowsMinLog ||
+                                                  LOGR > kRowsMaxLog || LOGR >= TL);
+  if constexpr (LOGR > MAXR || ROWS_OFF || ((KIND == KIND_STOCKHAM || KIND == KIND_DIT) && !HasStockham<E>::value)) {
     return hipErrorInvalidValue;
   } else {
     constexpr int TE = (KIND == KIND_SINGLE) ? (1 << LOGR) : (1 << TL);
@@ -2016,10 +2027,14 @@ static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassAr
       }
     }
     if (A.src2 || A.tw_in) return hipErrorInvalidValue;
-    if constexpr (KIND == KIND_COLUMN || KIND == KIND_STOCKHAM || KIND == KIND_DIT) {
-      if (A.tw_full) return launch_fsm<E, KIND, LOGR, true, false>(src, dst, A, g, b, st);
+    if constexpr (KIND == KIND_ROWS) {
+      return hipErrorInvalidValue;  // fast reductions only (the caller runs KIND_SINGLE otherwise)
+    } else {
+      if constexpr (KIND == KIND_COLUMN || KIND == KIND_STOCKHAM || KIND == KIND_DIT) {
+        if (A.tw_full) return launch_fsm<E, KIND, LOGR, true, false>(src, dst, A, g, b, st);
+      }
+      return launch_fsm<E, KIND, LOGR, false, false>(src, dst, A, g, b, st);
     }
-    return launch_fsm<E, KIND, LOGR, false, false>(src, dst, A, g, b, st);
   }
 }
 
@@ -2052,6 +2067,10 @@ hipError_t launch_pass(int kind, int logr, const uint32_t* src, uint32_t* dst, c
       if (kind == KIND_DIT) return launch_pass_kind<E, KIND_DIT>(logr, src, dst, A, grid, batch, st);
       return launch_pass_kind<E, KIND_STOCKHAM>(logr, src, dst, A, grid, batch, st);
     }
+    return hipErrorInvalidValue;
+  }
+  if (kind == KIND_ROWS) {  // grid = batch / (TILE / 2^logr) workgroups, batch argument 1
+    if constexpr (HasRows<E>::value) return launch_pass_kind<E, KIND_ROWS>(logr, src, dst, A, grid, batch, st);
     return hipErrorInvalidValue;
   }
   return launch_pass_kind<E, KIND_SINGLE>(logr, src, dst, A, grid, batch, st);

@@ -1181,7 +1181,28 @@ struct PlanImpl final : PlanBase {
       set_fs(A, FS_MAP_IN | FS_MAP_OUT);
       if (io) A.tw_epi = static_cast<const uint32_t*>(io->tw_epi);
       set_extents(A, io, il);
-      e = launch_pass<E>(KIND_SINGLE, (int)r[0], in, out, A, 1, il ? (1u << il) : batch, st);
+      const uint32_t nt = il ? (1u << il) : batch;  // transforms of this launch
+      // KIND_ROWS: TILE / n transforms per workgroup (the final pass's block layout: wave-uniform trivial
+      // twiddles, 4-wave workgroups) when the engine has it and the count divides; NTT_ROWS=0: one per
+      // workgroup (KIND_SINGLE)
+      const unsigned rows_log = (unsigned)tile_log_of<E>() - r[0];
+      static const bool rows_env = [] {
+        const char* v = getenv("NTT_ROWS");
+        return !(v && *v == '0');
+      }();
+      bool rows = false;
+      if constexpr (HasRows<E>::value)
+        rows = rows_env && Ff.red_ok && r[0] >= (unsigned)kRowsMinLog && r[0] <= (unsigned)kRowsMaxLog &&
+               rows_log >= 1 && nt >= (1u << rows_log) && (nt & ((1u << rows_log) - 1)) == 0;
+      if (rows) {
+        if (!il) {  // the transform index is part of every position: extents over the whole batch
+          if (A.dbg_src_n != ~(size_t)0) A.dbg_src_n = (size_t)n * batch;
+          if (A.dbg_dst_n != ~(size_t)0) A.dbg_dst_n = (size_t)n * batch;
+        }
+        e = launch_pass<E>(KIND_ROWS, (int)r[0], in, out, A, nt >> rows_log, 1, st);
+      } else {
+        e = launch_pass<E>(KIND_SINGLE, (int)r[0], in, out, A, 1, nt, st);
+      }
       mark(st);
     } else {
       if (il) batch = 1;  // Mode I: the 2^il interleaved transforms are one long column sweep

@@ -54,6 +54,24 @@ for s in $ARGS; do
         step rl_sh_default_$i 300 python3 -u tools/exp_ranklocal.py --out $O/rl_sh_default_$i.jsonl
         step rl_sh_off_$i 300 env NTT_SHOUP_OUTER=1 python3 -u tools/exp_ranklocal.py --out $O/rl_sh_off_$i.jsonl
       done ;;
+    rows_t) step pytest_rows 600 $PYT tests/test_gpu_rows.py tests/test_gpu_distributed.py tests/test_gpu_polymul_dist.py tests/test_gpu_mplan_copy.py tests/test_gpu_debug_build.py ;;
+    rows_b) RB="--cfg f1_L4_n3_b15 --cfg f1_L4_n4_b15 --cfg f1_L4_n5_b15 --cfg f1_L4_n6_b15 --cfg f1_L4_n7_b15 --cfg f1_L4_n7_inv_b15 --cfg f2_L4_n7_b15"
+      for i in 1 2; do
+        step batchs_rows_on_$i 200 python3 -u tools/exp_launches.py $RB --warmup 30 --steps 100 --out $O/batchs_rows_on_$i.jsonl
+        step batchs_rows_off_$i 200 env NTT_ROWS=0 python3 -u tools/exp_launches.py $RB --warmup 30 --steps 100 --out $O/batchs_rows_off_$i.jsonl
+      done ;;
+    rows_ab) # KIND_ROWS (several row transforms per workgroup) against NTT_ROWS=0 (one per workgroup), twice:
+      # rank-local four-step launches at G = 1..8 and batched short transforms
+      RB="--cfg f1_L4_n8_b15 --cfg f1_L4_n8_inv_b15 --cfg f1_L4_n7_b15 --cfg f1_L4_n9_b14 --cfg f1_L4_n6_b15"
+      [ -n "$RB_CFG" ] && RB="$RB_CFG"
+      for i in 1 2; do
+        step rl_rows_on_$i 300 python3 -u tools/exp_ranklocal.py --out $O/rl_rows_on_$i.jsonl
+        step rl_rows_off_$i 300 env NTT_ROWS=0 python3 -u tools/exp_ranklocal.py --out $O/rl_rows_off_$i.jsonl
+        step batch_rows_on_$i 200 python3 -u tools/exp_launches.py $RB --warmup 30 --steps 100 --out $O/batch_rows_on_$i.jsonl
+        step batch_rows_off_$i 200 env NTT_ROWS=0 python3 -u tools/exp_launches.py $RB --warmup 30 --steps 100 --out $O/batch_rows_off_$i.jsonl
+      done
+      step rl_rows_on_inv 300 python3 -u tools/exp_ranklocal.py --inverse --out $O/rl_rows_on_inv.jsonl
+      step rl_rows_off_inv 300 env NTT_ROWS=0 python3 -u tools/exp_ranklocal.py --inverse --out $O/rl_rows_off_inv.jsonl ;;
     prof_configs) step rocprof_configs 900 rocprofv3 --kernel-trace --stats -d $O/prof_configs -o run --output-format csv -- python3 tools/bench_configs.py --out $O/configs_traced.jsonl ;;
     pmc_rl) step pmc_ranklocal 900 env O=$O/pmc_rl bash tools/pmc_ranklocal.sh ;;
     rivals) step rivals 600 python3 -u tools/bench_rivals.py --out $O/rivals.jsonl ;;
