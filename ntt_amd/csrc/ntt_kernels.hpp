@@ -22,7 +22,7 @@ template <class E>
 struct HasStockham {
   static constexpr bool value = false;
 };
-// engines with KIND_ROWS instances (ntt_e256_rows.hip) and the radices they cover
+// engines with KIND_ROWS instances (ntt_e256_rows.hip, ntt_e256w_rows.hip) and the radices they cover
 template <class E>
 struct HasRows {
   static constexpr bool value = false;
@@ -54,6 +54,10 @@ struct HasStockham<EngP> {
 };
 template <>
 struct HasRows<Eng256> {
+  static constexpr bool value = true;
+};
+template <>
+struct HasRows<Eng256w> {  // the 6 x 64-bit layout of 256-bit moduli (BLS12-381 C3), ntt_e256w_rows.hip
   static constexpr bool value = true;
 };
 

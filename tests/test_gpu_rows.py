@@ -13,7 +13,7 @@ from oracle import oracle_c as OC
 
 pytestmark = pytest.mark.gpu
 
-TILE_LOG = 10  # Eng256's tile: 1024 elements
+TILE_LOG = 10  # the 256-bit engines' tile: 1024 elements
 
 
 def _plan(fid, log_n, L):
@@ -51,7 +51,7 @@ def _check_batch(fid, L, log_n, batch, x):
         assert np.array_equal(got[s * n:(s + 1) * n], exp), ("inverse", fid, log_n, batch, s)
 
 
-@pytest.mark.parametrize("fid,L", [(1, 4), (2, 4)])
+@pytest.mark.parametrize("fid,L", [(1, 4), (2, 4), (2, 6)])  # (2, 6): the 48-B layout engine
 @pytest.mark.parametrize("log_n", [3, 4, 5, 6, 7, 8, 9])
 def test_rows_batch_vs_oracle(fid, L, log_n):
     per_wg = 1 << (TILE_LOG - log_n)
