@@ -37,13 +37,14 @@ def _eq_at(t, src, idx, chunk=1 << 22):
                           (4, 22, 1, 4, 2, 1), (8, 24, 1, 4, 1, 1), (2, 22, 2, 6, 1, 1), (1, 26, 1, 4, 1, 1),
                           (2, 12, 1, 4, 1, 4), (2, 12, 1, 4, 4, 4), (8, 20, 1, 4, 4, 4), (4, 16, 1, 4, 2, 8),
                           (2, 14, 0, 1, 2, 2), (8, 16, 2, 6, 2, 2), (4, 22, 1, 4, 4, 4), (2, 24, 1, 4, 2, 2),
-                          (1, 26, 1, 4, 4, 8)])
+                          (1, 26, 1, 4, 4, 8), (2, 21, 1, 4, 1, 1), (4, 21, 1, 4, 2, 2)])
 def test_virtual_ranks_match_single_gpu(world, log_n, field_id, L, pieces, col_pieces, batched):
     """batched: each exchange unit's copies as one multi-tensor copy.  pieces / col_pieces > 1: the pipelined schedule (the exchange units copied on a side stream
     while the row transforms before them and the column transforms after them run) -- same column
     layout, same round trip.  2^22 / 2^24 / 2^26: the rank plans' unbalanced split (n2 = 2^10, one
     workgroup tile per row transform); 2^26 at world 1 has 2^16 rows per rank, launched in chunks of
-    2^15 (grid.y)."""
+    2^15 (grid.y).  2^21 splits 14 + 7: 2^7-point rows, eight per workgroup (KIND_ROWS) with the Mode B
+    output map and the epilogue table; 2^12 (6 + 6) takes KIND_ROWS in Mode I too."""
     from ntt_amd.distributed import VirtualRanks
     from ntt_amd.ntt import NTTPlan
     ref = NTTPlan(field_id, log_n, L)
@@ -92,10 +93,10 @@ def test_piece_entry_points_reject_bad_pieces():
 def test_rank_plan_split_takes_fewest_passes():
     """ntt_rplan_create's split: fewest pass kernels, then the smallest largest radix, then the most
     balanced (round 5).  2^24 BN254: 16 + 8 (2 + 1 passes of radix <= 2^8; 12 + 12 takes 2 + 2, 14 + 10
-    has a radix-2^10 row pass); 2^22: 14 + 8; 2^20 keeps 10 + 10 (1 + 1); C4's 2^28 keeps 14 + 14,
+    has a radix-2^10 row pass); 2^22: 14 + 8; 2^21: 14 + 7; 2^20 keeps 10 + 10 (1 + 1); C4's 2^28 keeps 14 + 14,
     asserted in test_gpu_fullsize."""
     from ntt_amd.distributed import RankPlan
-    for log_n, world, n2 in ((24, 1, 8), (24, 8, 8), (22, 2, 8), (20, 4, 10), (16, 2, 8)):
+    for log_n, world, n2 in ((24, 1, 8), (24, 8, 8), (22, 2, 8), (20, 4, 10), (16, 2, 8), (21, 2, 7)):
         rp = RankPlan(1, log_n, 4, world, 0, 0)
         assert (rp.layout.log_n1, rp.layout.log_n2) == (log_n - n2, n2), log_n
         del rp
