@@ -92,3 +92,26 @@ def test_rows_large_batch_round_trip(log_n):
         assert np.array_equal(got[s * n:(s + 1) * n], OC.ntt_mp(x[s * n:(s + 1) * n], p, g, False)), s
     pl.inverse_batch(t, batch)
     assert np.array_equal(_host(t, L), x)
+
+
+@pytest.mark.parametrize("fid,L", [(1, 4), (2, 6)])
+def test_rows_montgomery_io(fid, L):
+    """NTT_PLAN_MONTGOMERY_IO through KIND_ROWS: every transform of the batch commutes with the
+    Montgomery map (forward(a R) = forward(a) R), and the inverse brings the batch back."""
+    from ntt_amd.ntt import NTTPlan
+    p, g = R.FIELDS[fid]
+    log_n = 6
+    n, batch = 1 << log_n, 2 << (TILE_LOG - 6)
+    pm = NTTPlan(field_id=fid, log_n=log_n, limbs64=L, device=0, montgomery_io=True)
+    vecs = [R.random_vector(fid, n, seed=1200 + s) for s in range(batch)]
+    words = lambda v: [(int(v) >> (64 * k)) & (2**64 - 1) for k in range(L)]
+    x = np.array([words(R.to_mont(v, p, L)) for vec in vecs for v in vec], dtype=np.uint64)
+    t = pm.empty(batch)
+    t.copy_(_to_dev(x, L))
+    pm.forward_batch(t, batch)
+    got = _host(t, L)
+    for s, vec in enumerate(vecs):
+        exp = np.array([words(R.to_mont(v, p, L)) for v in R.ntt_dit(vec, p, g)], dtype=np.uint64)
+        assert np.array_equal(got[s * n:(s + 1) * n], exp), (fid, s)
+    pm.inverse_batch(t, batch)
+    assert np.array_equal(_host(t, L), x)
