@@ -36,7 +36,7 @@ SOURCES += ["ntt_e256t_fused.hip"]  # the two-pass single launch on 4096-element
 SOURCES += [f"ntt_{e}_{k}.hip" for e in ("e384", "e256", "e256w", "ep") for k in ("col", "single", "fin", "misc")]
 SOURCES += ["ntt_e256_stk.hip", "ntt_ep_stk.hip"]  # the bellperson-family rival schedule (NTT_PLAN_STOCKHAM)
 SOURCES += ["ntt_e256_dit.hip", "ntt_ep_dit.hip"]  # the GZKP(B, G) rival schedule (NTT_PLAN_GZKP)
-SOURCES += ["ntt_e256_rows.hip", "ntt_e256w_rows.hip"]  # batched single-tile transforms, several per workgroup (KIND_ROWS)
+SOURCES += ["ntt_e256_rows.hip", "ntt_e256w_rows.hip", "ntt_ep_rows.hip"]  # batched single-tile transforms, several per workgroup (KIND_ROWS)
 SOURCES += [f"ntt_epi_{k}.hip" for k in ("col", "single", "fin", "misc")]  # P with 8-B scratch (NTT_PLAN_IN_PLACE)
 SOURCES += [f"ntt_e256wi_{k}.hip" for k in ("col", "single", "fin", "misc")]  # 48-B in place (NTT_PLAN_IN_PLACE)
 SOURCES += [f"ntt_e256t_{k}.hip" for k in ("col", "single", "fin", "misc")]  # 4096-element tiles (2^20 single transforms)

@@ -12,22 +12,30 @@ namespace ntt {
 // permutation (ntt_plan_create_ex flag NTT_PLAN_STOCKHAM).
 // KIND_DIT: the GZKP(B, G) rival (GZKP-NTT.cu:115-165): in-place DIT column passes with input-side
 // twiddles w_N^(c d) over bit-reversed data (ntt_plan_create_ex flag NTT_PLAN_GZKP).
-// KIND_ROWS: a batch of short single-tile transforms (n <= 2^7), TILE / n of them per 4-wave workgroup
-// (the final pass's block layout), instead of one per workgroup (KIND_SINGLE, below one wave for
-// these n): batched short transforms and the four-step's row transforms (ntt_rplan) of such n.  At
-// n = 2^8 / 2^9 one transform per one- / two-wave workgroup is as fast or faster.
+// KIND_ROWS: a batch of short single-tile transforms (below one wave each: n <= 2^7 on the 256-bit
+// engines, 2^6 on P), TILE / n of them per workgroup (the final pass's block layout), instead of one
+// per workgroup (KIND_SINGLE): batched short transforms and the four-step's row transforms
+// (ntt_rplan) of such n.  At n = 2^8 / 2^9 on the 256-bit engines one transform per one- / two-wave
+// workgroup is as fast or faster.
 enum : int { KIND_COLUMN = 0, KIND_FINAL = 1, KIND_SINGLE = 2, KIND_STOCKHAM = 3, KIND_DIT = 4, KIND_ROWS = 5 };
 // engines with KIND_STOCKHAM instances (ntt_e256_stk.hip, ntt_ep_stk.hip)
 template <class E>
 struct HasStockham {
   static constexpr bool value = false;
 };
-// engines with KIND_ROWS instances (ntt_e256_rows.hip, ntt_e256w_rows.hip) and the radices they cover
+// engines with KIND_ROWS instances (ntt_e256_rows.hip, ntt_e256w_rows.hip, ntt_ep_rows.hip) and the radices they cover
 template <class E>
 struct HasRows {
   static constexpr bool value = false;
 };
-constexpr int kRowsMinLog = 3, kRowsMaxLog = 7;
+constexpr int kRowsMinLog = 3;
+// the largest KIND_ROWS radix of an engine, measured (profiles/r05_rows/): 2^7 on the
+// 256-bit engines (1024-element tiles, 256-thread workgroups); 2^6 on P, whose 8192-element tiles
+// make 1024-thread workgroups that lose to one transform per workgroup from 2^7 up (+20 %, 2^8 +180 %)
+template <class E>
+constexpr int rows_max_log() {
+  return E::W == 1 ? 6 : 7;
+}
 
 // Elements per workgroup tile of the multi-pass kernels (engines.hpp: E::TILE_LOG, E::EPT per thread).
 template <class E>
@@ -58,6 +66,10 @@ struct HasRows<Eng256> {
 };
 template <>
 struct HasRows<Eng256w> {  // the 6 x 64-bit layout of 256-bit moduli (BLS12-381 C3), ntt_e256w_rows.hip
+  static constexpr bool value = true;
+};
+template <>
+struct HasRows<EngP> {  // P469762049 (the reference's own field), ntt_ep_rows.hip
   static constexpr bool value = true;
 };
 

@@ -1992,9 +1992,10 @@ static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassAr
                                 uint32_t batch, hipStream_t st) {
   constexpr int TL = tile_log_of<E>();
   constexpr int MAXR = (KIND == KIND_SINGLE || KIND == KIND_ROWS) ? TL : TL - E::MIN_COLS_LOG;
-  // KIND_ROWS: the engines and radices ntt_e256_rows.hip instantiates (>= 2 transforms per tile), FAST only
-  constexpr bool ROWS_OFF = KIND == KIND_ROWS && (!HasRows<E>::value || !E::FASTRED || LOGR < kRowsMinLog ||
-                                                  LOGR > kRowsMaxLog || LOGR >= TL);
+  // KIND_ROWS: the engines and radices the ntt_*_rows.hip units instantiate (>= 2 transforms per tile);
+  // the quotient-estimate engines only in their FAST form
+  constexpr bool ROWS_OFF = KIND == KIND_ROWS && (!HasRows<E>::value || LOGR < kRowsMinLog ||
+                                                  LOGR > rows_max_log<E>() || LOGR >= TL);
   if constexpr (LOGR > MAXR || ROWS_OFF || ((KIND == KIND_STOCKHAM || KIND == KIND_DIT) && !HasStockham<E>::value)) {
     return hipErrorInvalidValue;
   } else {
@@ -2027,7 +2028,7 @@ static hipError_t launch_pass_r(const uint32_t* src, uint32_t* dst, const PassAr
       }
     }
     if (A.src2 || A.tw_in) return hipErrorInvalidValue;
-    if constexpr (KIND == KIND_ROWS) {
+    if constexpr (KIND == KIND_ROWS && E::FASTRED) {
       return hipErrorInvalidValue;  // fast reductions only (the caller runs KIND_SINGLE otherwise)
     } else {
       if constexpr (KIND == KIND_COLUMN || KIND == KIND_STOCKHAM || KIND == KIND_DIT) {

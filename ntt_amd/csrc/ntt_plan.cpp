@@ -1191,9 +1191,12 @@ struct PlanImpl final : PlanBase {
         return !(v && *v == '0');
       }();
       bool rows = false;
-      if constexpr (HasRows<E>::value)
-        rows = rows_env && Ff.red_ok && r[0] >= (unsigned)kRowsMinLog && r[0] <= (unsigned)kRowsMaxLog &&
+      if constexpr (HasRows<E>::value) {
+        bool fast_ok = true;  // the quotient-estimate engines run KIND_ROWS in their FAST form only
+        if constexpr (E::FASTRED) fast_ok = Ff.red_ok != 0;
+        rows = rows_env && fast_ok && r[0] >= (unsigned)kRowsMinLog && r[0] <= (unsigned)rows_max_log<E>() &&
                rows_log >= 1 && nt >= (1u << rows_log) && (nt & ((1u << rows_log) - 1)) == 0;
+      }
       if (rows) {
         if (!il) {  // the transform index is part of every position: extents over the whole batch
           if (A.dbg_src_n != ~(size_t)0) A.dbg_src_n = (size_t)n * batch;

@@ -115,3 +115,24 @@ def test_rows_montgomery_io(fid, L):
         assert np.array_equal(got[s * n:(s + 1) * n], exp), (fid, s)
     pm.inverse_batch(t, batch)
     assert np.array_equal(_host(t, L), x)
+
+
+@pytest.mark.parametrize("log_n", [3, 5, 6, 7, 9])
+def test_rows_p_field_vs_oracle(log_n):
+    """P469762049 (8-B elements, 8192-element tiles): KIND_ROWS up to 2^6 points; 2^7 and up keep one
+    transform per workgroup.  Every transform against the reference-pinned C oracle, both directions."""
+    from ntt_amd.ntt import NTTPlan
+    p, g = R.FIELDS[0]
+    n = 1 << log_n
+    per_wg = 1 << (13 - log_n)
+    pl = NTTPlan(field_id=0, log_n=log_n, limbs64=1, device=0)
+    for batch in (per_wg, 2 * per_wg + 1):
+        x = np.concatenate([OC.random_limbs(0, n, seed=3000 * log_n + s, L=1)[:, 0] for s in range(batch)])
+        x = x.astype(np.int64) % p  # canonical inputs (as test_gpu_parity does for P)
+        t = torch.from_numpy(x.copy()).to("cuda:0")
+        pl.forward_batch(t, batch)
+        got = t.cpu().numpy()
+        for s in range(batch):
+            assert np.array_equal(got[s * n:(s + 1) * n], OC.ntt_u64(x[s * n:(s + 1) * n], p, g)), (log_n, batch, s)
+        pl.inverse_batch(t, batch)
+        assert np.array_equal(t.cpu().numpy(), x), (log_n, batch)
