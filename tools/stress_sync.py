@@ -1,5 +1,5 @@
 """Stress of the inter-workgroup hand-offs (k_final_ipn: the in-place plans' fused digit reversal;
-k_fused3: NTT_PLAN_SINGLE_LAUNCH): many transforms of fresh random vectors through each, every output
+k_fused3 / k_fused3b / k_fused2b / k_fused2bi: NTT_PLAN_SINGLE_LAUNCH): many transforms of fresh random vectors through each, every output
 compared with the default schedule's and the watchdog status checked, so that a rare ordering race
 would show as a mismatch.
 
@@ -15,9 +15,12 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+# flags joined by '+' (round 5: the two-pass single launch at 2^20, k_fused2b, and its in-place form
+# k_fused2bi; BLS12-381 too)
 CASES = [(1, 20, 4, "in_place"), (1, 24, 4, "in_place"), (0, 22, 1, "in_place"), (0, 26, 1, "in_place"),
          (2, 22, 4, "in_place"), (1, 18, 4, "single_launch"), (1, 20, 4, "single_launch"),
-         (2, 22, 4, "single_launch")]
+         (2, 22, 4, "single_launch"), (1, 20, 4, "in_place+single_launch"), (2, 20, 4, "single_launch"),
+         (2, 20, 4, "in_place+single_launch"), (1, 19, 4, "in_place+single_launch")]
 
 
 def main():
@@ -30,7 +33,7 @@ def main():
     rows = []
     for fid, lg, limbs, flag in CASES:
         ref = NTTPlan(fid, lg, limbs)
-        pl = NTTPlan(fid, lg, limbs, **{flag: True})
+        pl = NTTPlan(fid, lg, limbs, **{f: True for f in flag.split("+")})
         bad = 0
         t0 = time.perf_counter()
         for rep in range(a.reps):
