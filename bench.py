@@ -117,6 +117,18 @@ def _cpu_share():
     return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail, avail
 
 
+def _cpu_model() -> str:
+    """The host CPU's model name (/proc/cpuinfo, SURVEY §8d: record the lscpu model)."""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.lower().startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
 def cpu_baseline(field_id: int, limbs: int, log_n: int):
     """The C oracle (oracle/ntt_oracle.c, a restatement of GZKP-NTT.cu:30-48) on the host: the full
     2^24 workload split over the box's CPU share (OpenMP, the multiprocess leg of SURVEY §8d), plus a
@@ -135,8 +147,9 @@ def cpu_baseline(field_id: int, limbs: int, log_n: int):
     t0 = time.perf_counter()
     OC.ntt_mp_par(xb, p, g, threads)
     dtp = time.perf_counter() - t0
-    cpu = platform.processor() or platform.machine()
+    cpu = _cpu_model()
     return {"value": (1 << big) / dtp, "unit": "field-elements/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu,
             "sample": f"one 2^{big}-point forward NTT ({FIELD_NAMES[field_id]}, {limbs}x64-bit limbs, SplitMix64 "
                       f"input) by the C oracle split over {threads} OpenMP threads ({cpu}): {dtp:.2f} s",
             "cores_note": f"{threads} threads = this process's CPU share (OMP_NUM_THREADS / affinity {avail}); "

@@ -64,3 +64,13 @@ def test_launcher_parent_never_loads_torch():
             "print('parent clean')\n" % ROOT)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "parent clean" in r.stdout, (r.stdout, r.stderr)
+
+
+def test_cpu_baseline_fields():
+    """The cpu_baseline object (§8d: the C oracle on the host's CPU share, the CPU model recorded) on a
+    small size: value, unit, cores, kind, sample, cpu_model, and the 1-core samples."""
+    import bench
+    cb = bench.cpu_baseline(1, 4, 10)
+    assert cb["value"] > 0 and cb["unit"] == "field-elements/s" and cb["kind"] == "port"
+    assert cb["cores"] >= 1 and isinstance(cb["cpu_model"], str) and cb["cpu_model"]
+    assert cb["single_core"]["cores"] == 1 and cb["reference_field_single_core"]["cores"] == 1
