@@ -116,7 +116,10 @@ struct Eng29 {
   static constexpr int TILE_LOG = TL_ ? TL_ : ((L <= 9) ? (EPT == 8 ? 11 : NTT_TILE_LOG_256) : 10);
   static constexpr int WAVES_PER_EU = (L <= 9) ? (EPT == 4 ? NTT_WAVES_256 : 2) : 2;
   static constexpr bool LDS_SPLIT = false;
-  static constexpr int MIN_COLS_LOG = 2;  // column passes own >= 4 adjacent columns: >= 128-B runs
+  // column passes own >= 4 adjacent columns: >= 128-B runs.  The 4096-element tiles also take one
+  // column per tile (radix 4096: 2^24 in two passes, 12 + 12, whose 32-B runs meet their three
+  // neighbours on one XCD through the XCD-grouped tile order; ntt_plan.cpp make_wide_plan)
+  static constexpr int MIN_COLS_LOG = TL_ == 12 ? 0 : 2;
   static constexpr bool PASS1_FULL_TABLE = NTT_256_PASS1_TABLE;  // VALU-bound: a table read beats a second product
   static constexpr bool NARROW_FIRST = false;  // near-equal radices
   // column passes after the first take their outer twiddles as Shoup pairs (w, ws) from L2-resident

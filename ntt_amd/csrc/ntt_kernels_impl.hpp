@@ -180,9 +180,14 @@ __device__ __forceinline__ void twiddle_mul_lds(uint32_t (&x)[E::W], const uint3
 #ifndef NTT_LDS_SWZ
 #define NTT_LDS_SWZ 0
 #endif
+// One column per tile (T = 1, radix 4096 on 4096-element tiles): consecutive lanes step pi by 1, 4, 16
+// or 64, so pi's 16-B slot is XOR-ed by bits 4..7 and 8..11 of pi (tools/lds_t1_sim.py: 0 extra
+// cycles per ds_read_b128 and 1.6 per ds_write_b128 against 26 / 22 unswizzled, measured 23).
 template <int T>
 __device__ __forceinline__ uint32_t lds_slot(uint32_t c, uint32_t pi) {
-  if constexpr (NTT_LDS_SWZ)
+  if constexpr (T == 1)
+    return pi ^ (((pi >> 4) ^ (pi >> 8)) & 15u);
+  else if constexpr (NTT_LDS_SWZ)
     return (c ^ (pi & (T - 1))) + T * (pi ^ ((pi >> 4) & 3));
   else
     return (c ^ (pi & (T - 1))) + T * pi;

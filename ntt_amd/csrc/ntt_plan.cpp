@@ -1277,15 +1277,21 @@ struct PlanImpl final : PlanBase {
       for (unsigned i = 0; i < npass; ++i) set_extents(PA[i], io, il);
       // XCD-grouped tile order (k_pass flag bit 2) for the column passes after the first whose runs are
       // shorter than a 128-B line (the 8-B path's 4-B scratch at radix 512: 64-B runs), so that the
-      // two tiles sharing each line meet on one XCD's L2.  NTT_XCD_ORDER=0 off, =1 on every pass.
+      // two tiles sharing each line meet on one XCD's L2.  Passes of one column per tile (radix 4096 on
+      // the 4096-element tiles) read and write 32-B runs, their final pass's stores too: every such
+      // pass takes the order, so the four tiles of each 128-B line run together.  NTT_XCD_ORDER=0 off,
+      // =1 on every column pass, =3 not on the one-column passes (A/B).
       static const int xcd_order = [] {
         const char* v = getenv("NTT_XCD_ORDER");
         return v && *v ? atoi(v) : 2;
       }();
       if (!io && xcd_order > 0)
-        for (unsigned i = 0; i + 1 < npass; ++i) {
-          const unsigned run_bytes = (1u << (tile_log_of<E>() - r[i])) * SCRW * 4;
-          if (xcd_order == 1 || (i > 0 && run_bytes < 128)) PA[i].flags |= 4u;
+        for (unsigned i = 0; i < npass; ++i) {
+          const unsigned cols = 1u << (tile_log_of<E>() - r[i]);
+          const unsigned run_bytes = cols * SCRW * 4;
+          const bool column = i + 1 < npass;
+          if ((column && (xcd_order == 1 || (i > 0 && run_bytes < 128))) || (cols == 1 && xcd_order != 3))
+            PA[i].flags |= 4u;
         }
       if constexpr (fused2_engine<E>()) {  // 2^20 on 4096-element tiles: the two-pass single launch
         if (!io && batch == 1 && npass == 2 && fused_enabled() && fused2_ready(PA, inplace)) {
@@ -1860,9 +1866,24 @@ static bool wide_flags_ok(unsigned flags) {
   const unsigned f = flags & ~NTT_PLAN_MONTGOMERY_IO;
   return f == 0 || f == NTT_PLAN_SINGLE_LAUNCH || f == (NTT_PLAN_SINGLE_LAUNCH | NTT_PLAN_IN_PLACE);
 }
+// 2^24 (the headline) on the same tiles in two passes, 12 + 12 with one column per column-pass tile:
+// one HBM round trip of the vector fewer than 8 + 8 + 8 on the 1024-element tiles.
+// NTT_TWO_PASS_24=1 routes a default 2^24 4-limb plan's single-vector transforms there.
+static bool two_pass_24_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("NTT_TWO_PASS_24");
+    return v && *v == '1';
+  }();
+  return on;
+}
 static void make_wide_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, const uint64_t* g64,
                            unsigned limbs64, unsigned log_n, int device, unsigned flags) {
-  if (limbs64 != 4 || log_n != 20 || !wide_flags_ok(flags) || !wide_tiles_enabled()) return;
+  if (limbs64 != 4 || !wide_flags_ok(flags) || !wide_tiles_enabled()) return;
+  if (log_n == 24) {
+    if (!two_pass_24_enabled() || (flags & ~NTT_PLAN_MONTGOMERY_IO)) return;
+  } else if (log_n != 20) {
+    return;
+  }
   if ((flags & NTT_PLAN_IN_PLACE) && (flags & NTT_PLAN_MONTGOMERY_IO)) return;
   uint32_t p32[12] = {0}, g32[12] = {0};
   for (unsigned i = 0; i < 4; ++i) {

@@ -128,6 +128,8 @@ def test_other_plans_keep_their_tiles():
     from ntt_amd.ntt import NTTPlan
     assert NTTPlan(1, 19, 4).passes == [7, 6, 6]
     assert NTTPlan(1, 21, 4).passes == [7, 7, 7]
+    if os.environ.get("NTT_TWO_PASS_24") != "1":  # the 12 + 12 A/B switch is off by default
+        assert NTTPlan(1, 24, 4).passes == [8, 8, 8]
     assert len(NTTPlan(1, 20, 4, in_place=True).passes) == 3
     # round 5: single-launch plans of 2^20 run the two passes as one launch (k_fused2b / k_fused2bi)
     assert NTTPlan(1, 20, 4, single_launch=True).passes == [10, 10]
@@ -151,6 +153,44 @@ def test_custom_modulus_plan_and_256_bit_shim_take_the_two_pass_plan():
     assert torch.equal(a, b) and torch.equal(a, c)
     custom.inverse(b)
     assert torch.equal(b, x)
+
+
+_CHILD_TWO_PASS = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+from ntt_amd.ntt import NTTPlan
+for fid in (1, 2):
+    pl = NTTPlan(fid, 24, 4)
+    assert pl.passes == [12, 12], pl.passes
+    n = pl.n
+    b = pl.empty(2)
+    bv = b.view(2, n, -1)
+    pl.fill(bv[0], "random", seed=61 + fid)
+    pl.fill(bv[1], "iota")
+    x0, x1 = bv[0].clone(), bv[1].clone()
+    pl.set_profiling(True)
+    pl.forward(x0)
+    assert len(pl.last_launch_ms()) == 2
+    pl.set_profiling(False)
+    pl.forward(x1)
+    pl.forward_batch(b, 2)  # 8 + 8 + 8 on the 1024-element tiles
+    assert torch.equal(bv[0], x0) and torch.equal(bv[1], x1), fid
+    pl.inverse(x0); pl.inverse(x1); pl.inverse_batch(b, 2)
+    assert torch.equal(bv[0], x0) and torch.equal(bv[1], x1), fid
+    assert pl.device_status() == 0
+print("child ok")
+"""
+
+
+def test_two_pass_24_switch_is_bit_exact():
+    """NTT_TWO_PASS_24=1 (an A/B switch: measured slower): a 2^24 4-limb
+    plan runs one vector's transforms as 12 + 12 on 4096-element tiles, one column per column-pass
+    tile.  Forward and inverse, BN254 and BLS12-381, bit for bit against the same plan's batched
+    8 + 8 + 8 path."""
+    env = dict(os.environ, NTT_TWO_PASS_24="1")
+    r = subprocess.run([sys.executable, "-c", _CHILD_TWO_PASS.format(root=ROOT)], env=env, capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0 and "child ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
 
 _CHILD_FAIL = r"""
