@@ -188,7 +188,24 @@ def load_traffic(tag: str):
         return None, f"no PMC summary for {tag}"
     if ent.get("src_hash") != source_hash():
         return None, f"stale: PMC summary measured on sources {ent.get('src_hash')}, current {source_hash()}"
-    return ent.get("launch_bytes"), ent.get("profile")
+    return ent, ent.get("profile")
+
+
+def pair_traffic(ent, labels, launch_ms):
+    """PMC bytes per launch of this run, paired by launch LABEL: the summary's
+    launches (tools/pmc_to_traffic.py: labels from the rocprofv3 kernel names) must be this run's
+    launches (ntt_plan_last_launch_labels), same labels in the same order, one timing per launch;
+    otherwise (None, reason) and no traffic is reported."""
+    if not isinstance(ent, dict):
+        return None, ent
+    lb, ll = ent.get("launch_bytes"), ent.get("launch_labels")
+    if not lb or ll is None:
+        return None, "PMC entry without per-launch labels"
+    if list(ll) != list(labels):
+        return None, f"PMC launches {list(ll)} are not this run's launches {list(labels)}"
+    if len(lb) != len(ll) or (launch_ms is not None and len(launch_ms) != len(ll)):
+        return None, f"{len(lb)} PMC launches, {len(ll)} labels, {len(launch_ms or [])} timed launches"
+    return list(lb), None
 
 
 def _free_port() -> int:
@@ -503,6 +520,7 @@ def main():
     barrier()
     t1 = time.perf_counter()
     launch_avg = plan_for_prof.last_launch_ms()  # per-launch average over the timed steps (<= 64)
+    launch_labels = plan_for_prof.last_launch_labels()  # which kernel each of those launches was
     plan_for_prof.set_profiling(False)
     exchange_ms = eng.exchange_ms() if four_step else None  # mean all-to-all window per step
 
@@ -586,7 +604,10 @@ def main():
     # kernels only -- the all-to-all's own HBM reads and writes are not in it)
     tag = (f"f{args.field}_L{args.limbs}_n{args.log_n}_w{gpus_per_transform}{'_fs' if four_step else ''}"
            f"{'_inv' if args.inverse else ''}")
-    launch_bytes, prof_src = load_traffic(tag)
+    ent, prof_src = load_traffic(tag)
+    launch_bytes, unpaired = pair_traffic(ent, launch_labels, launch_avg)
+    if launch_bytes is None and isinstance(ent, dict):
+        prof_src = f"{prof_src}: not attached, {unpaired}"
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": (sum(launch_bytes) if launch_bytes else None),
@@ -601,11 +622,14 @@ def main():
         local_n = n // world if four_step else n
         alg_bytes = 2 * local_n * elem_bytes
         ach_k = alg_bytes / (launch_avg[k] * 1e-3) / 1e9
-        roof["dominant_kernel"] = {"kernel": f"launch {k} of {len(launch_avg)}", "kernel_ms": launch_avg[k],
+        roof["dominant_kernel"] = {"kernel": f"launch {k} of {len(launch_avg)}" +
+                                             (f" ({launch_labels[k]})" if k < len(launch_labels) else ""),
+                                   "kernel_ms": launch_avg[k],
                                    "achieved": ach_k, "frac": ach_k / HBM_PEAK_GBPS,
                                    "algorithmic_bytes_per_launch": alg_bytes,
                                    "traffic": (launch_bytes[k] if launch_bytes and k < len(launch_bytes) else None)}
         roof["launch_ms"] = launch_avg
+        roof["launch_labels"] = launch_labels
         if launch_bytes and len(launch_bytes) == len(launch_avg):
             out["hbm_pmc_gbps_per_gpu"] = sum(launch_bytes) / (sum(launch_avg) * 1e-3) / 1e9
         if args.limbs == 4 and args.field in (1, 2) and not four_step and len(passes) == len(launch_avg) \

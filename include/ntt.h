@@ -238,6 +238,18 @@ int ntt_transpose_ex(ntt_plan* plan, const void* d_src, void* d_dst, unsigned lo
  * schedule the most recent call ran (single-vector or batched, see ntt_plan_info). */
 int ntt_plan_set_profiling(ntt_plan* plan, int enable);
 int ntt_plan_last_launch_ms(ntt_plan* plan, float* ms, unsigned max_launches, unsigned* nlaunches);
+/* The same launches' labels, comma-separated, in launch order: a kind letter and the pass's log2
+ * radix (c column pass, "s" appended when it reads a Shoup-pair outer table; f final pass; s one
+ * transform per workgroup; r several per workgroup; i in-place final pass with the digit reversal;
+ * d digit-reversal swap; b single launch; n naive), "" when unlabelled.  NTT_ERR_ARG when `cap`
+ * bytes do not hold them.  New (round 6): benchmarks pair per-launch PMC bytes with launches by
+ * label, not by position. */
+int ntt_plan_last_launch_labels(ntt_plan* plan, char* buf, unsigned cap);
+/* Group mode: from this call on, the plan's transforms accumulate into ONE record (timings and
+ * labels) until the next call, so that ntt_plan_last_launch_ms reports every launch of a caller-level
+ * operation made of several transforms (the rank plan's row transforms of 2^15 rows each); the time
+ * between two transforms of a group is not reported. */
+int ntt_plan_profile_group(ntt_plan* plan);
 
 /* Plan introspection: n, bytes per element, number of passes and their log2 radices (of a
  * single-vector transform: a default or Montgomery-I/O 4 x 64-bit plan of exactly 2^20 runs those on
@@ -329,6 +341,11 @@ int ntt_rplan_fill(ntt_rplan* rp, void* d_x, int kind, uint64_t seed, void* hip_
 /* per-launch timing of the row (which = 0) or column (1) transforms, as ntt_plan_last_launch_ms */
 int ntt_rplan_set_profiling(ntt_rplan* rp, int enable);
 int ntt_rplan_last_launch_ms(ntt_rplan* rp, int which, float* ms, unsigned max_launches, unsigned* nlaunches);
+int ntt_rplan_last_launch_labels(ntt_rplan* rp, int which, char* buf, unsigned cap);
+/* the row and column plans' group mode (ntt_plan_profile_group): call at the start of every four-step
+ * transform, so that the timings report each of its launches (e.g. the row transform's launches of
+ * 2^15 rows each at world size 1) */
+int ntt_rplan_profile_group(ntt_rplan* rp);
 int ntt_rplan_destroy(ntt_rplan* rp);
 
 /* ---------------------------------------------------------------- single-process multi-GPU

@@ -11,12 +11,6 @@
 #include "field29.hpp"
 #include "field29_asm9.hpp"
 
-// timing-only experiment builds (never the product): bit 0 drops the reductions, bit 1 the Shoup
-// products, bit 2 the Montgomery products, bit 3 the carry normalisations, bit 4 folds the first
-// pass's n-entry outer-twiddle table reads into an L2-resident window (tools/r03_ab.sh)
-#ifndef NTT_AB_SKIP
-#define NTT_AB_SKIP 0
-#endif
 // Debug build (ntt_amd/libntt_debug.so, NTT_DEBUG_CHECKS=1): the pass kernels check every HBM index
 // against its buffer, the caller's inputs for canonical form, the lazy bound (< 2p) of every
 // intermediate and the canonical form of every output, and record violations in a per-plan status
@@ -185,7 +179,7 @@ struct Eng29 {
   template <int FROM, int TO>
   __device__ static __forceinline__ void reduce_chain(uint32_t (&x)[W], const Args& A) {
     static_assert(FROM <= 32 && TO >= 1, "lazy bound");
-    if constexpr (FROM > TO && !(NTT_AB_SKIP & 1)) {
+    if constexpr (FROM > TO) {
       constexpr int j = __builtin_ctz(FROM / 2);
       cond_sub<L>(x, A.kp[j]);
       reduce_chain<FROM / 2, TO>(x, A);
@@ -204,9 +198,6 @@ struct Eng29 {
   // 128-VGPR cap, where the 32-bit form spills and measured 3.6 % slower in pass 1).
   template <bool R32 = true>
   __device__ static __forceinline__ void reduce_top(uint32_t (&x)[W], const Args& A) {
-#if NTT_AB_SKIP & 1
-    return;  // timing-only experiment build (tools/r03_ab.sh): results are wrong
-#endif
     const float qf = __builtin_fmaf((float)x[L - 1], A.red_inv, -0x1p-15f);
     const uint32_t q = qf > 0.f ? (uint32_t)qf : 0u;
     if constexpr (R32) {
@@ -232,9 +223,6 @@ struct Eng29 {
   // x < 2q (normalised) -> x < q, skipping the subtraction when no lane of the wave can need it
   // (top limb below q's: x < q for sure).  Wave-uniform branch.
   __device__ static __forceinline__ void cond_sub_rare(uint32_t (&x)[W], const uint32_t (&q)[L]) {
-#if NTT_AB_SKIP & 1
-    return;
-#endif
     if (__any(x[L - 1] >= q[L - 1])) cond_sub<L>(x, q);
   }
   template <int FROM, int TO, bool FAST = false, bool R32 = true>
@@ -300,11 +288,7 @@ struct Eng29 {
   __device__ static __forceinline__ void mul(uint32_t (&x)[W], const Tw& t, const Args& A) {
     uint32_t r[W];
     if constexpr (L == 9)
-#if NTT_AB_SKIP & 2
-      for (int i = 0; i < W; ++i) r[i] = x[i] ^ t.w[i];
-#else
       mulc29_a9(r, x, t.w, t.ws, A.pbar);
-#endif
     else
       mulc29_blk<L>(r, x, t.w, t.ws, A.pbar);
 #pragma unroll
@@ -315,11 +299,7 @@ struct Eng29 {
   __device__ static __forceinline__ void mul_u(uint32_t (&x)[W], const Tw& t, const Args& A) {
     uint32_t r[W];
     if constexpr (L == 9)
-#if NTT_AB_SKIP & 2
-      for (int i = 0; i < W; ++i) r[i] = x[i] ^ t.w[i];
-#else
       mulc29_a9u(r, x, t.w, t.ws, A.pbar);
-#endif
     else
       mulc29_blk<L>(r, x, t.w, t.ws, A.pbar);
 #pragma unroll
@@ -329,11 +309,7 @@ struct Eng29 {
   __device__ static __forceinline__ void mulv(uint32_t (&x)[W], const uint32_t (&y)[W], const Args& A) {
     uint32_t r[W];
     if constexpr (L == 9)
-#if NTT_AB_SKIP & 4
-      for (int i = 0; i < W; ++i) r[i] = x[i] ^ y[i];
-#else
       mont29_a9(r, x, y, A.M);
-#endif
     else
       mont29<L>(r, x, y, A.M);
 #pragma unroll
@@ -347,10 +323,8 @@ struct Eng29 {
       a[i] = x + y;
       b[i] = x - y + q[i];
     }
-#if !(NTT_AB_SKIP & 8)
     norm_u<L>(a);
     norm_s<L>(b);
-#endif
   }
   template <int K>
   __device__ static __forceinline__ void bfly_l(uint32_t (&a)[W], uint32_t (&b)[W], const Args& A) {
@@ -380,9 +354,7 @@ struct Eng29 {
     mul_u(b, t, A);  // t: one of the w_8^k kernel arguments
   }
   __device__ static __forceinline__ void norm(uint32_t (&x)[W]) {
-#if !(NTT_AB_SKIP & 8)
     norm_u<L>(x);
-#endif
   }
 };
 

@@ -183,12 +183,13 @@ struct FusedArgs {
   uint32_t dbg;                // diagnostics only (NTT_FUSED_DBG): bit 0 no dependency waits (wrong
                                // output), bit 2 static tile order (needs every workgroup resident)
   uint32_t mode;               // 0: dataflow hand-offs between tiles (k_fused3); 1: two grid barriers
-                               // over a cooperative launch (k_fused3b); 2: the NTT_PLAN_IN_PLACE form,
-                               // three grid barriers, one workgroup per tile (k_fused3bi); 3: two passes
-                               // on 4096-element tiles, one barrier (k_fused2b); 4: the same in place,
-                               // two barriers (k_fused2bi)
+                               // (k_fused3b); 2: the NTT_PLAN_IN_PLACE form, residency + three grid
+                               // barriers, one workgroup per tile (k_fused3bi); 3: two passes on
+                               // 4096-element tiles, one barrier (k_fused2b); 4: the same in place,
+                               // residency + two barriers (k_fused2bi)
   Watchdog wd;                 // bounded waits
-  uint32_t* shards;            // grid barriers (modes 1, 2): 8 arrival shards, one 128-B line each
+  uint32_t* shards;            // grid barriers (modes 1..4): 8 arrival shards, one 128-B line each
+  unsigned long long* trace;   // diagnostics (NTT_FUSED_TRACE, modes 3 and 4): 4 timestamps per workgroup
 };
 template <class E>
 hipError_t launch_fused3(int r1, int r2, int r3, const uint32_t* src, uint32_t* scratch, uint32_t* dst,

@@ -24,19 +24,6 @@
 
 namespace ntt {
 
-// Diagnostic build (-DNTT_DEBUG_NOMEM=1, never the product): every pass-kernel data / table access
-// folded into a 16-Ki-element window, so the kernels run from L2 -- their time without HBM traffic
-// (2^24 BN254: 1.29 ms instead of 1.67 ms, i.e. ~23 % of the time is HBM not hidden behind VALU).
-#if NTT_DEBUG_NOMEM
-#define NTT_NOMEM(i) ((i) & ((size_t)(1u << 14) - 1))
-#else
-#define NTT_NOMEM(i) (i)
-#endif
-// Timing experiments only: wave priority (s_setprio) for a tile's load phase (bit 0; bit 2:
-// not in a pass that reads the caller's buffer) and for its output phase (bit 1).
-#ifndef NTT_PRIO
-#define NTT_PRIO 0
-#endif
 
 // Compile-time loop: f(std::integral_constant<int, I>{}) for I in [0, N).  Register arrays indexed
 // by I stay in VGPRs (a loop the unroller gives up on would send x[][] to scratch).
@@ -174,12 +161,9 @@ __device__ __forceinline__ void twiddle_mul_lds(uint32_t (&x)[E::W], const uint3
 
 // LDS slot of (local column/block c, in-column position pi): column-minor like HBM, with c XOR-ed
 // by the low bits of pi so that both lane orders used (c fastest, or pi fastest) hit distinct
-// 16-byte slots (the final pass writes with pi fastest: 8-way conflicts without the swizzle).
-// NTT_LDS_SWZ=1 also XORs pi's low 2 bits with bits 4..5 (tools/lds_sim.py swz_hi: fewer read
-// conflicts for the wave-uniform sub-stage mapping below).
-#ifndef NTT_LDS_SWZ
-#define NTT_LDS_SWZ 0
-#endif
+// 16-byte slots (the final pass writes with pi fastest: 8-way conflicts without the swizzle).  A
+// swizzle that also removed the wave-uniform sub-stage's read conflicts cost more address VALU than
+// the conflicts (+0.8 %).
 // One column per tile (T = 1, radix 4096 on 4096-element tiles): consecutive lanes step pi by 1, 4, 16
 // or 64, so pi's 16-B slot is XOR-ed by bits 4..7 and 8..11 of pi (tools/lds_t1_sim.py: 0 extra
 // cycles per ds_read_b128 and 1.6 per ds_write_b128 against 26 / 22 unswizzled, measured 23).
@@ -187,8 +171,6 @@ template <int T>
 __device__ __forceinline__ uint32_t lds_slot(uint32_t c, uint32_t pi) {
   if constexpr (T == 1)
     return pi ^ (((pi >> 4) ^ (pi >> 8)) & 15u);
-  else if constexpr (NTT_LDS_SWZ)
-    return (c ^ (pi & (T - 1))) + T * (pi ^ ((pi >> 4) & 3));
   else
     return (c ^ (pi & (T - 1))) + T * pi;
 }
@@ -397,12 +379,71 @@ __device__ __forceinline__ bool grid_barrier_words(uint32_t* top, uint32_t* shar
   __syncthreads();
   return __builtin_amdgcn_readfirstlane(s_ok) != 0u;
 }
-// The in-place single launch's last barrier (the K-th of the launch: 3 in k_fused3bi, 2 in
+// The in-place single launch's last barrier (the K-th of the launch: 4 in k_fused3bi, 3 in
 // k_fused2bi), between every final tile's loads and any store (PassArgs: ipn_sync = the top counter,
 // ipn_shards = the shard lines, ipn_go = the go word)
 template <uint32_t K, class E>
 __device__ __forceinline__ bool ipn_grid_barrier(const PassArgs<E>& A) {
   return grid_barrier_words(A.ipn_sync, A.ipn_shards, A.ipn_go, K, A.wd);
+}
+
+// Residency of an in-place single launch (k_fused2bi, k_fused3bi).  Their grid barriers need every
+// workgroup resident at once, which a plain launch promises only on a device nobody else holds CUs of
+// (another process, or a persistent kernel of the caller's on another stream).  Were a workgroup left
+// waiting for a CU, the resident ones would trip the watchdog after pass 1 had already overwritten the
+// caller's buffer.  So every workgroup arrives at kernel start (grid barrier 1 of the launch, no wait),
+// and before its FIRST store waits until all G have arrived.  The go word is decided once, by
+// compare-exchange: the last arrival sets it 0 -> 1 (go), a waiter whose bounded poll ran out sets it
+// 0 -> 2 (abandon: no workgroup of the launch stores anything, the caller's buffer is unchanged, and
+// the call is reported through the watchdog as NTT_ERR_DEVICE).  Arriving costs one atomic per
+// workgroup; the wait is normally satisfied at its first poll, a whole pass-1 tile after the last
+// workgroup started.
+__device__ __forceinline__ void residency_arrive(uint32_t* top, uint32_t* shards, uint32_t* go) {
+  if (threadIdx.x == 0) {
+    const uint32_t G = gridDim.x, sh = blockIdx.x & 7u;
+    const uint32_t ns = (G + 7u - sh) >> 3, nsh = G < 8u ? G : 8u;
+    if (__hip_atomic_fetch_add(shards + 32 * sh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ns - 1 &&
+        __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsh - 1) {
+      uint32_t zero = 0u;
+      __hip_atomic_compare_exchange_strong(go, &zero, 1u, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+// True (workgroup-uniform) when the launch's go word says go; false when it was abandoned.
+__device__ __forceinline__ bool residency_wait(uint32_t* go, const Watchdog& wd) {
+  __shared__ uint32_t s_go;
+  if (threadIdx.x == 0) {
+    typedef __attribute__((address_space(1))) uint32_t gu32;
+    uint32_t v = 0;
+    for (uint32_t spins = 0;; ++spins) {
+      v = __hip_atomic_load((gu32*)go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v) break;
+      if (spins >= wd.spins) {
+        uint32_t cur = 0u;
+        if (__hip_atomic_compare_exchange_strong(go, &cur, 2u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          watchdog_trip(wd);
+          v = 2u;
+        } else {
+          v = cur;  // decided meanwhile
+        }
+        break;
+      }
+      if (spins < 16) __builtin_amdgcn_s_sleep(4);
+      else __builtin_amdgcn_s_sleep(32);
+    }
+    s_go = v;
+  }
+  __syncthreads();
+  return __builtin_amdgcn_readfirstlane(s_go) == 1u;
+}
+// Once a workgroup has passed its residency_wait the go word is final (1 or 2) until the launch's
+// last workgroup out clears it: the kernel reads the decision there.
+__device__ __forceinline__ bool residency_went(uint32_t* go) {
+  __shared__ uint32_t s_go;
+  if (threadIdx.x == 0) s_go = __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  return __builtin_amdgcn_readfirstlane(s_go) == 1u;
 }
 
 // LDS of one pass tile (words), and whether the pass stages its w_R^e table in LDS: E::LDS_TW
@@ -430,8 +471,9 @@ __host__ __device__ constexpr bool pass_ltw() {
 // VGPRs across the whole loop, they spilled 200-380 B per thread; per tile they cost a few VALU ops).
 // IPN (final pass of an in-place plan): outputs go to their natural positions in the same buffer.
 // 1 (k_final_ipn): a tile's loads are counted in per slab, and its stores wait until the mirror slab
-// has been read.  2 (k_fused3bi, every final tile resident): a grid barrier between all loads and all
-// stores.
+// has been read.  2 / 3 (k_fused3bi / k_fused2bi, every final tile resident): a grid barrier between
+// all loads and all stores.  4 (pass 1 of k_fused3bi / k_fused2bi): the stores wait for the launch's
+// residency decision (residency_wait) and are skipped when it was abandoned.
 template <class E, int LOGR, int KIND, bool FULLTW, bool FAST, int PRO = PRO_NONE, bool SRC_USER = true,
           int FSM = 0, bool SHTW = false, bool WT = false, bool LOOPED = false, int IPN = 0>
 __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
@@ -459,13 +501,6 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
   int t = threadIdx.x;
   if constexpr (LOOPED) asm volatile("" : "+v"(t));
   if (t >= NT) return;
-#if NTT_PRIO & 1
-  // timing experiment: a new tile's address math and loads issue ahead of older waves' compute
-  __builtin_amdgcn_s_setprio(2);
-#elif NTT_PRIO & 4
-  // the same except in a pass that reads the caller's buffer (pass 1: it measured slower there)
-  if (!(KIND == KIND_COLUMN && A.src_user)) __builtin_amdgcn_s_setprio(2);
-#endif
   // Four-step addressing (PassArgs::fs, ntt_rplan_*): the first pass may read and the last pass may
   // write through the per-peer chunk maps, and Mode I runs 2^il interleaved transforms.  All flags
   // are kernel arguments (wave-uniform branches); fs == 0 is the plain batched transform.
@@ -595,7 +630,7 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
           pos = pi;
         }
         const size_t b = ROWS ? (size_t)w * T + c : (size_t)bq;  // this element's transform
-        E::template load<SW>(x[j * Q + d], src, ck(NTT_NOMEM(IN_USER ? in_pos(pos, b) : pos), A.dbg_src_n));
+        E::template load<SW>(x[j * Q + d], src, ck(IN_USER ? in_pos(pos, b) : pos, A.dbg_src_n));
 #if NTT_DEBUG_CHECKS
         // the caller's elements must be canonical (the reference's BAD LIMB trap); a column pass reads
         // them only when A.src_user (one SRC_USER instance also serves later passes when the scratch
@@ -624,9 +659,6 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
         }
       });
     });
-#if NTT_PRIO & 5
-    __builtin_amdgcn_s_setprio(0);  // the tile's loads are issued
-#endif
     static_for<G>([&](auto J) {
       constexpr int j = J;
       dft<E, Q, j * Q, FAST>(x, A.F);
@@ -661,12 +693,11 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
   // ------------------------------------------------------------------ output
   if constexpr (IPN == 1) {  // the slab this tile writes into has been read (or the wait gave up: no stores)
     if (!ipn_wait_mirror(A, midrev)) return;
-  } else if constexpr (IPN >= 2) {  // in-place single launch: every final tile has read (grid barrier)
-    if (!ipn_grid_barrier<IPN == 2 ? 3u : 2u>(A)) return;
+  } else if constexpr (IPN == 2 || IPN == 3) {  // in-place single launch: every final tile has read (grid barrier)
+    if (!ipn_grid_barrier<IPN == 2 ? 4u : 3u>(A)) return;
+  } else if constexpr (IPN == 4) {  // in-place single launch, pass 1: every workgroup is resident (A.ipn_go)
+    if (!residency_wait(A.ipn_go, A.wd)) return;
   }
-#if NTT_PRIO & 2
-  __builtin_amdgcn_s_setprio(1);  // timing experiment: finishing tiles drain first
-#endif
   {
     constexpr int ls = S::nsub - 1;
     constexpr int qb = S::qb(ls), Q = 1 << qb, G = EPT / Q, sb = S::logsig(ls), lN = S::logN(ls);
@@ -684,12 +715,12 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
         if constexpr (KIND == KIND_DIT) {
           // in place (GZKP-NTT.cu:157-158): output k of column c back to c + s k of its block
           pos = colbase + c + ((size_t)kn << log_s);
-          E::template store<E::IN * Q, FAST, DW>(dst, ck(NTT_NOMEM(pos), A.dbg_dst_n), v, A.F);
+          E::template store<E::IN * Q, FAST, DW>(dst, ck(pos, A.dbg_dst_n), v, A.F);
         } else if constexpr (KIND == KIND_STOCKHAM) {
           // autosort store (GZKP-NTT.cu:378-384): y[((index - k) << deg) + k + kn p], k = index mod p
           const uint32_t idx = col0 + c, kk = idx & ((1u << A.lgp) - 1);
           pos = ((size_t)(idx - kk) << LOGR) + kk + ((size_t)kn << A.lgp);
-          E::template store<E::IN * Q, FAST, DW>(dst, ck(NTT_NOMEM(pos), A.dbg_dst_n), v, A.F);
+          E::template store<E::IN * Q, FAST, DW>(dst, ck(pos, A.dbg_dst_n), v, A.F);
         } else if constexpr (KIND == KIND_COLUMN) {
           if constexpr (FULLTW) {
             // outer twiddle w_{N_i}^{col * kn} R_e from the per-pass table (HBM element format,
@@ -704,13 +735,10 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
             }
             if constexpr (SHTW) {  // Shoup pair (w, floor(w B / p)), E::TW words: 143 MADs, no R_e
               typename E::Tw tws;
-              E::tload(tws, A.tw_full, NTT_NOMEM(ti));
+              E::tload(tws, A.tw_full, ti);
               E::mul(v, tws, A.F);
             } else {
-#if NTT_AB_SKIP & 16  // timing-only (tools/r03_ab.sh): the table reads folded into an L2-resident window
-              ti &= (size_t(1) << 14) - 1;
-#endif
-              E::template load<E::TABW>(tw, A.tw_full, NTT_NOMEM(ti));
+              E::template load<E::TABW>(tw, A.tw_full, ti);
               E::mulv(v, tw, A.F);
             }
           } else {
@@ -724,7 +752,7 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
             E::mulv(v, tl.w, A.F);
           }
           pos = colbase + c + ((size_t)kn << log_s);
-          E::template store_lazy<E::MUL_OUT, FAST, DW, WT>(dst, ck(NTT_NOMEM(pos), A.dbg_dst_n), v, A.F);  // scratch: < 2p, read by the next pass
+          E::template store_lazy<E::MUL_OUT, FAST, DW, WT>(dst, ck(pos, A.dbg_dst_n), v, A.F);  // scratch: < 2p, read by the next pass
         } else if constexpr (KIND == KIND_FINAL) {
           if (fs_il) {
             const uint32_t k1 = k10 + (c >> tb_log), b = b0 + (c & ((1u << tb_log) - 1));
@@ -738,9 +766,9 @@ __device__ __forceinline__ void pass_tile(const uint32_t* __restrict__ src, uint
             uint32_t tw[E::W];
             E::template load<E::TABW>(tw, A.tw_epi, epi_idx(pos, bq));
             E::mulv(v, tw, A.F);
-            E::template store<E::MUL_OUT, FAST, DW>(dst, ck(NTT_NOMEM(out_pos(pos, bq)), A.dbg_dst_n), v, A.F);
+            E::template store<E::MUL_OUT, FAST, DW>(dst, ck(out_pos(pos, bq), A.dbg_dst_n), v, A.F);
           } else {
-            E::template store<E::IN * Q, FAST, DW>(dst, ck(NTT_NOMEM(out_pos(pos, bq)), A.dbg_dst_n), v, A.F);
+            E::template store<E::IN * Q, FAST, DW>(dst, ck(out_pos(pos, bq), A.dbg_dst_n), v, A.F);
           }
         } else {  // KIND_SINGLE, KIND_ROWS
           pos = kn;
@@ -1018,7 +1046,7 @@ void k_fused3(const FusedKArgs<E> K) {
 }
 
 // The same three passes with two grid-wide barriers instead of per-tile hand-offs (FusedArgs::mode 1,
-// a cooperative launch, so every workgroup is resident).  Each workgroup runs tiles b, b + G, ... of a
+// a plain launch of at most the workgroups the device holds at once).  Each workgroup runs tiles b, b + G, ... of a
 // pass, then the barrier.  The barrier (the guide's R1 publish, MI355X_MICROARCH.md § visibility):
 // * scratch stores are write-through (sc1), so no release fence: every wave drains them, then a
 //   workgroup barrier, then one lane counts the workgroup in;
@@ -1082,7 +1110,9 @@ void k_fused3b(const FusedKArgs<E> K) {
 // schedule writes its outputs to their natural positions, which lie in the mirror slab, so every final
 // tile loads and transforms, a third grid barrier makes sure every tile has read, and only then do the
 // tiles store (IPN = 2 in pass_tile).  That needs every final tile resident at once: one tile per
-// workgroup, nwg == tiles (n <= 2^20 at 4 workgroups per CU), a cooperative launch.
+// workgroup, nwg == tiles (n <= 2^20 at 4 workgroups per CU), and a residency check before the first
+// store (residency_arrive / residency_wait: barrier 1), so that a launch whose workgroups are not all
+// resident stores nothing.
 template <class E, int R1, int R2, int R3>
 __global__ __launch_bounds__((1 << E::TILE_LOG) / E::EPT) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
 void k_fused3bi(const FusedKArgs<E> K) {
@@ -1093,31 +1123,33 @@ void k_fused3bi(const FusedKArgs<E> K) {
   __shared__ uint32_t lds_tw[1];
   const FusedArgs& F = K.F;
   const uint32_t G = gridDim.x;
-  for (uint32_t w = blockIdx.x; w < F.tiles; w += G) {  // pass 1, in place
+  uint32_t* const go1 = F.sync + F.rbase;  // residency: grid barrier 1 (residency_arrive)
+  residency_arrive(F.sync, F.shards, go1);
+  for (uint32_t w = blockIdx.x; w < F.tiles; w += G) {  // pass 1, in place; its stores wait for residency
     const FusedKArgs<E>& L = fused_kargs<E>();
-    pass_tile<E, R1, KIND_COLUMN, true, true, PRO_NONE, true, 0, false, true, true>(L.dst, L.dst, L.A1, w, 0, lds,
-                                                                                      lds_tw);
+    pass_tile<E, R1, KIND_COLUMN, true, true, PRO_NONE, true, 0, false, true, true, 4>(L.dst, L.dst, L.A1, w, 0, lds,
+                                                                                         lds_tw);
     __syncthreads();
   }
-  bool ok = fused_grid_barrier(F, 1);
+  bool ok = residency_went(go1) && fused_grid_barrier(F, 2);
   for (uint32_t w = blockIdx.x; ok && w < F.tiles; w += G) {  // pass 2, in place
     const FusedKArgs<E>& L = fused_kargs<E>();
     pass_tile<E, R2, KIND_COLUMN, true, true, PRO_NONE, true, 0, true, true, true>(L.dst, L.dst, L.A2, w, 0, lds,
                                                                                      lds_tw);
     __syncthreads();
   }
-  ok = ok && fused_grid_barrier(F, 2);
-  if (ok && blockIdx.x < F.tiles) {  // final pass: load, transform, barrier 3 (inside), natural-order stores
+  ok = ok && fused_grid_barrier(F, 3);
+  if (ok && blockIdx.x < F.tiles) {  // final pass: load, transform, barrier 4 (inside), natural-order stores
     const FusedKArgs<E>& L = fused_kargs<E>();
     pass_tile<E, R3, KIND_FINAL, false, true, PRO_NONE, true, 0, false, false, true, 2>(L.dst, L.dst, L.A3,
                                                                                          blockIdx.x, 0, lds, lds_tw);
   }
   if (threadIdx.x == 0 && __hip_atomic_fetch_add(F.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
-    // the last workgroup out: every other one has passed (or given up at) all three barriers
+    // the last workgroup out: every other one has passed (or given up at) all four barriers
     __hip_atomic_store(F.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(F.sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (F.wd.abort) __hip_atomic_store(F.wd.abort, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (uint32_t k = 0; k < 3; ++k)
+    for (uint32_t k = 0; k < 4; ++k)
       __hip_atomic_store(F.sync + F.rbase + 32 * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (uint32_t sh = 0; sh < 8; ++sh) __hip_atomic_store(F.shards + 32 * sh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -1132,10 +1164,16 @@ void k_fused3bi(const FusedKArgs<E> K) {
 // ends in NTT_ERR_DEVICE, never a hang.
 //   k_fused2b  (FusedArgs::mode 3): pass 1 caller -> scratch (write-through), barrier, final pass
 //              scratch -> caller, natural order.
-//   k_fused2bi (FusedArgs::mode 4): NTT_PLAN_IN_PLACE, the palindromic 10 + 10: pass 1 in place,
-//              barrier 1, the final pass loads and transforms every tile, barrier 2 (every tile has
-//              read: all 256 final tiles are resident), then the stores to the natural positions in the
-//              mirror slab (pass_tile IPN = 3).  No scratch.
+//   k_fused2bi (FusedArgs::mode 4): NTT_PLAN_IN_PLACE, the palindromic 10 + 10: pass 1 in place (its
+//              stores wait for the residency decision, barrier 1), barrier 2, the final pass loads and
+//              transforms every tile, barrier 3 (every tile has read: all 256 final tiles are
+//              resident), then the stores to the natural positions in the mirror slab (pass_tile
+//              IPN = 3).  No scratch.
+// FusedArgs::trace (diagnostics, NTT_FUSED_TRACE): per workgroup the wall clock (100 MHz) at start,
+// after pass 1, after the pass barrier and at the end.
+__device__ __forceinline__ void fused_trace(const FusedArgs& F, uint32_t at) {
+  if (F.trace && threadIdx.x == 0) F.trace[4 * blockIdx.x + at] = (unsigned long long)wall_clock64();
+}
 template <class E, int R1, int R2>
 __global__ __launch_bounds__((1 << E::TILE_LOG) / E::EPT) __attribute__((amdgpu_waves_per_eu(E::WAVES_PER_EU)))
 void k_fused2b(const FusedKArgs<E> K) {
@@ -1146,19 +1184,23 @@ void k_fused2b(const FusedKArgs<E> K) {
   __shared__ uint32_t lds_tw[1];
   const FusedArgs& F = K.F;
   const uint32_t G = gridDim.x;
+  fused_trace(F, 0);
   for (uint32_t w = blockIdx.x; w < F.tiles; w += G) {  // pass 1: the caller's buffer -> scratch
     const FusedKArgs<E>& L = fused_kargs<E>();
     pass_tile<E, R1, KIND_COLUMN, true, true, PRO_NONE, true, 0, false, true, true>(L.src, L.scratch, L.A1, w, 0, lds,
                                                                                       lds_tw);
     __syncthreads();
   }
+  fused_trace(F, 1);
   const bool ok = fused_grid_barrier(F, 1);
+  fused_trace(F, 2);
   for (uint32_t w = blockIdx.x; ok && w < F.tiles; w += G) {  // final pass: scratch -> the caller's buffer
     const FusedKArgs<E>& L = fused_kargs<E>();
     pass_tile<E, R2, KIND_FINAL, false, true, PRO_NONE, true, 0, false, false, true>(L.scratch, L.dst, L.A3, w, 0, lds,
                                                                                       lds_tw);
     __syncthreads();
   }
+  fused_trace(F, 3);
   if (threadIdx.x == 0 && __hip_atomic_fetch_add(F.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
     // the last workgroup out: every other one has passed (or given up at) the barrier
     __hip_atomic_store(F.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1179,23 +1221,29 @@ void k_fused2bi(const FusedKArgs<E> K) {
   __shared__ uint32_t lds_tw[1];
   const FusedArgs& F = K.F;
   const uint32_t G = gridDim.x;
-  for (uint32_t w = blockIdx.x; w < F.tiles; w += G) {  // pass 1, in place
+  uint32_t* const go1 = F.sync + F.rbase;  // residency: grid barrier 1 (residency_arrive)
+  fused_trace(F, 0);
+  residency_arrive(F.sync, F.shards, go1);
+  for (uint32_t w = blockIdx.x; w < F.tiles; w += G) {  // pass 1, in place; its stores wait for residency
     const FusedKArgs<E>& L = fused_kargs<E>();
-    pass_tile<E, R, KIND_COLUMN, true, true, PRO_NONE, true, 0, false, true, true>(L.dst, L.dst, L.A1, w, 0, lds,
-                                                                                     lds_tw);
+    pass_tile<E, R, KIND_COLUMN, true, true, PRO_NONE, true, 0, false, true, true, 4>(L.dst, L.dst, L.A1, w, 0, lds,
+                                                                                        lds_tw);
     __syncthreads();
   }
-  const bool ok = fused_grid_barrier(F, 1);
-  if (ok && blockIdx.x < F.tiles) {  // final pass: load, transform, barrier 2 (inside), natural-order stores
+  fused_trace(F, 1);
+  const bool ok = residency_went(go1) && fused_grid_barrier(F, 2);
+  fused_trace(F, 2);
+  if (ok && blockIdx.x < F.tiles) {  // final pass: load, transform, barrier 3 (inside), natural-order stores
     const FusedKArgs<E>& L = fused_kargs<E>();
     pass_tile<E, R, KIND_FINAL, false, true, PRO_NONE, true, 0, false, false, true, 3>(L.dst, L.dst, L.A3, blockIdx.x, 0,
                                                                                         lds, lds_tw);
   }
+  fused_trace(F, 3);
   if (threadIdx.x == 0 && __hip_atomic_fetch_add(F.sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
     __hip_atomic_store(F.sync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(F.sync + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (F.wd.abort) __hip_atomic_store(F.wd.abort, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (uint32_t k = 0; k < 2; ++k)
+    for (uint32_t k = 0; k < 3; ++k)
       __hip_atomic_store(F.sync + F.rbase + 32 * k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (uint32_t sh = 0; sh < 8; ++sh) __hip_atomic_store(F.shards + 32 * sh, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -1245,22 +1293,14 @@ hipError_t launch_fused3(int r1, int r2, int r3, const uint32_t* src, uint32_t* 
   } else {
     const dim3 g(F.nwg), b((1 << E::TILE_LOG) / E::EPT);
     FusedKArgs<E> K{src, scratch, dst, A1, A2, A3, F};
-    void* kargs[] = {&K};
-    // Round 5: the grid-barrier forms are PLAIN launches by default, after the plan's occupancy check
-    // that the grid fits the device (fused3_capacity).  hipLaunchCooperativeKernel cost ~20 us per call
-    // (DESIGN §4), and every rocprofv3-traced process that made one crashed in the runtime's exit
-    // handlers ("exit-time SIGSEGV").  NTT_FUSED_COOP=1: the cooperative launch (which
-    // guarantees co-residency even beside other persistent kernels).
-    static const bool coop = [] {
-      const char* v = getenv("NTT_FUSED_COOP");
-      return v && *v == '1';
-    }();
-    // mode 1: with NTT_FUSED_COOP=1 a cooperative launch (every workgroup resident, or the launch fails)
-    if (F.mode == 2) {  // in place: cooperative launch of exactly one workgroup per tile
+    // The grid-barrier forms are plain launches of at most the occupancy query's workgroups (the plan
+    // checks that the grid fits the device, fused3_capacity); the plan serialises its single launches
+    // per device (ntt_plan.cpp FusedSerial), and the in-place form checks residency before its first
+    // store.  Round 6 retired the cooperative launch: ~20 us more per call, and every
+    // rocprofv3-traced process that had made one crashed in the runtime's exit handlers.
+    if (F.mode == 2) {  // in place: one workgroup per tile
 #define NTT_FUSED_IP_CASE(a, c, d)                                                                \
   if (r1 == a && r2 == c && r3 == d) {                                                            \
-    if (coop)                                                                                     \
-      return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_fused3bi<E, a, c, d>), g, b, kargs, 0, st); \
     hipLaunchKernelGGL((k_fused3bi<E, a, c, d>), g, b, 0, st, K);                                 \
     return hipGetLastError();                                                                     \
   }
@@ -1272,8 +1312,6 @@ hipError_t launch_fused3(int r1, int r2, int r3, const uint32_t* src, uint32_t* 
     }
 #define NTT_FUSED_CASE(a, c, d)                                                                   \
   if (r1 == a && r2 == c && r3 == d) {                                                            \
-    if (F.mode == 1 && coop)                                                                      \
-      return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&k_fused3b<E, a, c, d>), g, b, kargs, 0, st); \
     if (F.mode == 1) {                                                                            \
       hipLaunchKernelGGL((k_fused3b<E, a, c, d>), g, b, 0, st, K);                                \
       return hipGetLastError();                                                                   \

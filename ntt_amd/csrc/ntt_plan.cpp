@@ -20,6 +20,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <tuple>
 #include <type_traits>
 #include <vector>
@@ -33,6 +34,75 @@ using namespace ntt;
 namespace {
 
 thread_local int g_last_error = NTT_OK;
+
+// ------------------------------------------------------------------------------ single-launch order
+// The single launches (k_fused3 / k_fused3b / k_fused3bi / k_fused2b / k_fused2bi) wait across
+// workgroups, so each assumes its workgroups own the device: two of them enqueued on two streams could
+// have their workgroups dispatched interleaved, each holding part of the CUs, and both would wait for
+// the other's workgroups until the watchdog gave up (NTT_ERR_DEVICE).  The library therefore orders
+// them per device, under one lock: a single launch on another stream than the device's previous one
+// first makes its stream wait for everything enqueued so far on that previous stream (an event
+// recorded there at this moment), which includes the previous single launch.  Launches on one stream
+// are in order already and pay nothing: an event recorded after every launch cost 4.5 us of device time
+// per call (a marker packet behind the kernel; profiles/r06_c2/).  A previous stream that has been
+// destroyed (hipStreamGetFlags fails) has finished its work.  Work of other kinds is not ordered.
+// (The in-place forms also check residency before their first store, for CUs held by anything else:
+// ntt_kernels_impl.hpp residency_wait.)
+class FusedSerial {
+ public:
+  FusedSerial(int device, hipStream_t st) : lk_(mu()), s_(enabled() ? slot(device) : nullptr), st_(st) {
+    if (!s_ || !s_->used || s_->last == st) return;
+    unsigned fl = 0;
+    if (hipStreamGetFlags(s_->last, &fl) != hipSuccess) {  // gone: its work is done
+      (void)hipGetLastError();
+      return;
+    }
+    if (!s_->ev && hipEventCreateWithFlags(&s_->ev, hipEventDisableTiming) != hipSuccess) {
+      s_->ev = nullptr;
+      (void)hipGetLastError();
+      return;
+    }
+    if (hipEventRecord(s_->ev, s_->last) == hipSuccess) (void)hipStreamWaitEvent(st, s_->ev, 0);
+  }
+  void done(hipError_t launched) {
+    if (!s_ || launched != hipSuccess) return;
+    s_->last = st_;
+    s_->used = true;
+  }
+
+ private:
+  struct Slot {
+    hipStream_t last = nullptr;  // the stream of the device's latest single launch
+    bool used = false;
+    hipEvent_t ev = nullptr;     // process-lifetime, like the plan cache
+  };
+  static bool enabled() {  // NTT_FUSED_ORDER=0: no ordering (A/B only)
+    static const bool on = [] {
+      const char* v = getenv("NTT_FUSED_ORDER");
+      return !(v && *v == '0');
+    }();
+    return on;
+  }
+  static std::mutex& mu() {
+    static std::mutex* m = new std::mutex;
+    return *m;
+  }
+  static Slot* slot(int device) {
+    static Slot* slots = new Slot[64];
+    return (device >= 0 && device < 64) ? &slots[device] : nullptr;
+  }
+  std::lock_guard<std::mutex> lk_;
+  Slot* s_;
+  hipStream_t st_;
+};
+
+// Diagnostics (NTT_FUSED_TRACE=<file>): the two-pass single launch writes per-workgroup wall-clock
+// stamps (start, after pass 1, after the barrier, end; 100 MHz), appended to <file> after each call,
+// which then synchronises its stream.  Never on in measured runs.
+static const char* fused_trace_path() {
+  static const char* p = getenv("NTT_FUSED_TRACE");
+  return (p && *p) ? p : nullptr;
+}
 
 // ------------------------------------------------------------------------------ host field math
 template <int N>
@@ -144,11 +214,20 @@ struct PlanBase {
   unsigned r[8] = {0};
   int device = 0;
   // optional per-launch timing: events recorded on the caller's stream between launches, one
-  // slot per transform in a ring of kSlots transforms (no host synchronisation per transform)
-  static constexpr unsigned kSlots = 64, kEv = 9;
+  // slot per transform in a ring of kSlots transforms (no host synchronisation per transform).
+  // Each interval between two events carries a label naming the launch it timed (kind letter +
+  // log2 radix, "s" for a Shoup-pair outer table: c8, c8s, f8, r8, s12, i8, d, b; tools/pmc_to_traffic.py
+  // derives the same labels from the rocprofv3 kernel names), "" when unlabelled.
+  // Grouping (ntt_plan_profile_group, the rank plan's four-step transforms): once a plan has been put
+  // in group mode, a transform continues the current slot until the next group call, so the slot holds
+  // every launch of one caller-level operation (e.g. a row transform run as two launches of 2^15 rows);
+  // the time between two transforms of a group is an interval labelled "-" and is not a launch.
+  static constexpr unsigned kSlots = 64, kEv = 17;
   bool profiling = false;
   hipEvent_t ev[kSlots][kEv] = {};
+  char lab[kSlots][kEv][6] = {};  // label of the interval that ends at event k
   unsigned ev_used = 0, slot = 0, nrec = 0;
+  bool grouped = false, group_new = false;
   // Watchdog report (ntt_kernels.hpp): a host-mapped word that a kernel sets when one of its bounded
   // inter-workgroup waits gives up.  Every later call on the plan returns NTT_ERR_DEVICE (a plain host
   // read, no device query) until ntt_plan_device_status reads and clears it.
@@ -165,13 +244,24 @@ struct PlanBase {
   bool alloc_watch();  // true once the plan holds a report word (defined after the slot pool)
   void begin(hipStream_t st) {
     if (!profiling) return;
+    if (grouped && !group_new && nrec > 0 && ev_used > 0 && ev_used + 1 < kEv) {
+      mark(st, "-");  // the same group: the time since its previous transform is a gap
+      return;
+    }
+    group_new = false;
     slot = nrec % kSlots;
     ev_used = 0;
     ++nrec;
     mark(st);
   }
-  void mark(hipStream_t st) {
-    if (profiling && ev_used < kEv) (void)hipEventRecord(ev[slot][ev_used++], st);
+  void mark(hipStream_t st, const char* kind = "", unsigned log_radix = 0, bool shoup = false) {
+    if (!profiling || ev_used >= kEv) return;
+    char* l = lab[slot][ev_used];
+    if (log_radix)
+      snprintf(l, sizeof lab[0][0], "%s%u%s", kind, log_radix, shoup ? "s" : "");
+    else
+      snprintf(l, sizeof lab[0][0], "%s", kind);
+    (void)hipEventRecord(ev[slot][ev_used++], st);
   }
 };
 
@@ -483,6 +573,7 @@ struct PlanImpl final : PlanBase {
     if (d_sync) (void)hipFree(d_sync);
     if (d_sync_ip) (void)hipFree(d_sync_ip);
     if (d_sync2) (void)hipFree(d_sync2);
+    if (d_trace) (void)hipFree(d_trace);
     if (d_ipn) (void)hipFree(d_ipn);
     if (d_pw) (void)hipFree(d_pw);
     if (d_dbg) (void)hipFree(d_dbg);
@@ -1173,7 +1264,7 @@ struct PlanImpl final : PlanBase {
       A.tw_int = d_tab + off_int[0];
       A.flags = inverse ? 1u : 0u;
       e = launch_naive<E>(in, out, A, batch, st);
-      mark(st);
+      mark(st, "n");
     } else if (npass == 1) {
       PassArgs<E> A = base_args(inverse);
       A.tw_int = d_tab + off_int[0];
@@ -1206,7 +1297,7 @@ struct PlanImpl final : PlanBase {
       } else {
         e = launch_pass<E>(KIND_SINGLE, (int)r[0], in, out, A, 1, nt, st);
       }
-      mark(st);
+      mark(st, rows ? "r" : "s", r[0]);
     } else {
       if (il) batch = 1;  // Mode I: the 2^il interleaved transforms are one long column sweep
       // NTT_PLAN_IN_PLACE (not for four-step pieces, whose passes map positions): every pass reads and
@@ -1297,18 +1388,27 @@ struct PlanImpl final : PlanBase {
         if (!io && batch == 1 && npass == 2 && fused_enabled() && fused2_ready(PA, inplace)) {
           FusedArgs F = inplace ? fargs2_ip : fargs2;
           F.wd = watchdog(F.wd.abort);
-          if (inplace) {  // k_fused2bi: the final pass's barrier is the launch's second
-            PassArgs<E> B = A;
-            B.flags &= ~2u;
-            B.ipn_sync = F.sync;
-            B.ipn_go = F.sync + F.rbase + 32;
-            B.ipn_shards = F.shards;
-            B.wd = F.wd;
-            e = launch_fused2<E>((int)r[0], (int)r[1], out, nullptr, out, PA[0], B, F, st);
-          } else {
-            e = launch_fused2<E>((int)r[0], (int)r[1], in, work, out, PA[0], A, F, st);
+          F.trace = fused_trace_buffer(F.nwg);
+          {
+            FusedSerial order(device, st);
+            if (inplace) {  // k_fused2bi: residency (barrier 1), pass barrier 2, the final pass's barrier 3
+              PassArgs<E> A1 = PA[0];
+              A1.ipn_go = F.sync + F.rbase;  // pass 1's stores wait for the residency decision
+              A1.wd = F.wd;
+              PassArgs<E> B = A;
+              B.flags &= ~2u;
+              B.ipn_sync = F.sync;
+              B.ipn_go = F.sync + F.rbase + 64;
+              B.ipn_shards = F.shards;
+              B.wd = F.wd;
+              e = launch_fused2<E>((int)r[0], (int)r[1], out, nullptr, out, A1, B, F, st);
+            } else {
+              e = launch_fused2<E>((int)r[0], (int)r[1], in, work, out, PA[0], A, F, st);
+            }
+            order.done(e);
           }
-          mark(st);
+          mark(st, "b");
+          if (F.trace && e == hipSuccess) dump_fused_trace(F, inplace, st);
           return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
         }
       }
@@ -1317,8 +1417,12 @@ struct PlanImpl final : PlanBase {
           // one persistent launch for the three passes (NTT_PLAN_SINGLE_LAUNCH, k_fused3)
           FusedArgs F = fused_args();
           F.wd = watchdog(F.wd.abort);
-          e = launch_fused3<E>((int)r[0], (int)r[1], (int)r[2], in, work, out, PA[0], PA[1], PA[2], F, st);
-          mark(st);
+          {
+            FusedSerial order(device, st);
+            e = launch_fused3<E>((int)r[0], (int)r[1], (int)r[2], in, work, out, PA[0], PA[1], PA[2], F, st);
+            order.done(e);
+          }
+          mark(st, "b");
           return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
         }
       }
@@ -1327,21 +1431,28 @@ struct PlanImpl final : PlanBase {
           // the in-place single launch (k_fused3bi): three passes in the caller's buffer, no scratch
           FusedArgs F = fargs_ip;
           F.wd = watchdog(F.wd.abort);
+          PassArgs<E> A1 = PA[0];
+          A1.ipn_go = F.sync + F.rbase;  // pass 1's stores wait for the residency decision (barrier 1)
+          A1.wd = F.wd;
           PassArgs<E> B = A;
           B.flags &= ~2u;
           B.ipn_sync = F.sync;
-          B.ipn_go = F.sync + F.rbase + 64;  // the third barrier's go word
+          B.ipn_go = F.sync + F.rbase + 96;  // the fourth barrier's go word
           B.ipn_shards = F.shards;           // its arrival shards (cumulative, like the top counter)
           B.wd = F.wd;
-          e = launch_fused3<E>((int)r[0], (int)r[1], (int)r[2], out, nullptr, out, PA[0], PA[1], B, F, st);
-          mark(st);
+          {
+            FusedSerial order(device, st);
+            e = launch_fused3<E>((int)r[0], (int)r[1], (int)r[2], out, nullptr, out, A1, PA[1], B, F, st);
+            order.done(e);
+          }
+          mark(st, "b");
           return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
         }
       }
       for (unsigned i = 0; i + 1 < npass && e == hipSuccess; ++i) {
         const uint32_t* src = (i == 0) ? in : work;
         e = launch_pass<E>(KIND_COLUMN, (int)r[i], src, work, PA[i], grid, batch, st);
-        mark(st);
+        mark(st, "c", r[i], PA[i].tw_sh != 0);
       }
       if (e == hipSuccess && inplace && batch == 1 && ipn_ready(A)) {
         // the final pass writes natural positions in place, the digit reversal fused (k_final_ipn)
@@ -1352,10 +1463,10 @@ struct PlanImpl final : PlanBase {
         B.ipn_strips = ipn_strips;
         B.wd = watchdog(d_ipn + 32 * (1 + ipn_slabs));
         e = launch_final_ipn<E>((int)r[npass - 1], out, B, grid, st);
-        mark(st);
+        mark(st, "i", r[npass - 1]);
       } else if (e == hipSuccess) {
         e = launch_pass<E>(KIND_FINAL, (int)r[npass - 1], work, out, A, grid, batch, st);
-        mark(st);
+        mark(st, "f", r[npass - 1]);
         if (inplace && e == hipSuccess) {
           DrevArgs D{};
           D.log_n = log_n;
@@ -1370,7 +1481,7 @@ struct PlanImpl final : PlanBase {
           }();
           D.diag = drev_diag ? 1u : 0u;
           e = launch_digitrev_swap<E>(out, D, batch, st);
-          mark(st);
+          mark(st, "d");
         }
       }
     }
@@ -1452,7 +1563,8 @@ struct PlanImpl final : PlanBase {
   // ---- the two-pass single launch on 4096-element tiles (NTT_PLAN_SINGLE_LAUNCH, 2^20 4-limb plans:
   // k_fused2b, and k_fused2bi in place; ntt_kernels_impl.hpp).  Plain launches of at most the occupancy
   // query's workgroups; the in-place form needs every one of the 256 final tiles resident.
-  // Sync words: [0] top arrivals, [1] exits; go words at 32, 64; abort at 96; shards at 128 + 32 s.
+  // Sync words: [0] top arrivals, [1] exits; go words at 32, 64, 96 (in place: residency, pass barrier,
+  // final barrier); abort at 128; shards at 160 + 32 s.
   uint32_t* d_sync2 = nullptr;
   FusedArgs fargs2{}, fargs2_ip{};
   int fused2_state[2] = {0, 0};  // [in place]: 0 not built, 1 ready, -1 unavailable
@@ -1472,12 +1584,12 @@ struct PlanImpl final : PlanBase {
       if (fused2_capacity<E>((int)r[0], (int)r[1], device, &cap, mode) != hipSuccess || cap == 0) return false;
       if (inplace && cap < tiles) return false;
       if (!d_sync2) {
-        if (hipMalloc(&d_sync2, 384 * 4) != hipSuccess) {
+        if (hipMalloc(&d_sync2, 416 * 4) != hipSuccess) {
           d_sync2 = nullptr;
           (void)hipGetLastError();
           return false;
         }
-        if (hipMemset(d_sync2, 0, 384 * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return false;
+        if (hipMemset(d_sync2, 0, 416 * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return false;
       }
       FusedArgs F{};
       F.tiles = tiles;
@@ -1485,13 +1597,36 @@ struct PlanImpl final : PlanBase {
       F.mode = mode;
       F.rbase = 32;
       F.sync = d_sync2;
-      F.wd.abort = d_sync2 + 96;
-      F.shards = d_sync2 + 128;
+      F.wd.abort = d_sync2 + 128;
+      F.shards = d_sync2 + 160;
       if (getenv("NTT_FUSED_VERBOSE"))
         fprintf(stderr, "libntt: two-pass single launch (mode %u), %u tiles per pass, %u workgroups (capacity %u)\n",
                 mode, tiles, F.nwg, cap);
       (inplace ? fargs2_ip : fargs2) = F;
       return true;
+    }
+  }
+  // NTT_FUSED_TRACE (diagnostics): the stamps buffer, and its dump after the call
+  unsigned long long* d_trace = nullptr;
+  unsigned long long* fused_trace_buffer(uint32_t nwg) {
+    if (!fused_trace_path()) return nullptr;
+    if (!d_trace && hipMalloc(&d_trace, (size_t)4 * 8 * 1024) != hipSuccess) {
+      d_trace = nullptr;
+      (void)hipGetLastError();
+    }
+    return (d_trace && nwg <= 1024) ? d_trace : nullptr;
+  }
+  void dump_fused_trace(const FusedArgs& F, bool inplace, hipStream_t st) {
+    std::vector<unsigned long long> h((size_t)4 * F.nwg);
+    if (hipStreamSynchronize(st) != hipSuccess ||
+        hipMemcpy(h.data(), F.trace, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess)
+      return;
+    if (FILE* f = fopen(fused_trace_path(), "a")) {
+      fprintf(f, "{\"kernel\": \"%s\", \"log_n\": %u, \"nwg\": %u, \"stamps\": [", inplace ? "k_fused2bi" : "k_fused2b",
+              log_n, F.nwg);
+      for (size_t i = 0; i < h.size(); ++i) fprintf(f, "%s%llu", i ? ", " : "", h[i]);
+      fprintf(f, "]}\n");
+      fclose(f);
     }
   }
   bool single_launch_ready() override {
@@ -1508,7 +1643,7 @@ struct PlanImpl final : PlanBase {
 
   // ---- the in-place single launch (NTT_PLAN_SINGLE_LAUNCH on an NTT_PLAN_IN_PLACE plan, k_fused3bi):
   // 3-pass palindromic FAST 256-bit schedules whose tiles all fit the device at once (2^18 .. 2^20)
-  uint32_t* d_sync_ip = nullptr;  // [0] top arrivals, [1] exits; go words at 32, 64, 96; abort at 128; shards at 160
+  uint32_t* d_sync_ip = nullptr;  // [0] top arrivals, [1] exits; go words at 32 (residency), 64, 96, 128; abort at 160; shards at 192
   FusedArgs fargs_ip{};
   bool fused_ip_built = false, fused_ip_ok = false;
   bool fused_ip_ready(const PassArgs<E>* PA) {
@@ -1534,15 +1669,15 @@ struct PlanImpl final : PlanBase {
       if (const char* v = getenv("NTT_FUSED_VERBOSE"))
         fprintf(stderr, "libntt: in-place single launch, %u tiles per pass, %u workgroups (capacity %u)\n", tiles,
                 tiles, cap);
-      // go words at 32, 64, 96; abort at 128; barrier shards at 160 + 32 s
-      if (hipMalloc(&d_sync_ip, 416 * 4) != hipSuccess) {
+      // go words at 32 (residency), 64, 96, 128; abort at 160; barrier shards at 192 + 32 s
+      if (hipMalloc(&d_sync_ip, 448 * 4) != hipSuccess) {
         d_sync_ip = nullptr;
         return false;
       }
-      if (hipMemset(d_sync_ip, 0, 416 * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return false;
+      if (hipMemset(d_sync_ip, 0, 448 * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return false;
       F.sync = d_sync_ip;
-      F.wd.abort = d_sync_ip + 128;
-      F.shards = d_sync_ip + 160;
+      F.wd.abort = d_sync_ip + 160;
+      F.shards = d_sync_ip + 192;
       fargs_ip = F;
       return true;
     }
@@ -1855,8 +1990,9 @@ static bool wide_tiles_enabled() {
 // failure may leak into the plan's calls.  A failed hipMalloc inside its init leaves the error as the
 // thread's last HIP error, which the next launch check (hipGetLastError) would return as NTT_ERR_HIP
 // from a healthy plan, so it is cleared here.  It is not attempted at all when the
-// device is short of memory (its scratch and tables take ~100 MiB at 2^20).  NTT_TEST_WIDE_FAIL=1
-// (tests only) makes the attempt fail through a refused allocation.
+// device is short of memory (its scratch and tables take ~100 MiB at 2^20).  In the checked build
+// (NTT_DEBUG_CHECKS, libntt_debug.so) only, NTT_TEST_WIDE_FAIL=1 makes the attempt fail through a
+// refused allocation (tests/test_gpu_wide_tiles.py); the product build has no such hook.
 static constexpr size_t kWideMinFreeBytes = 512ull << 20;
 // NTT_PLAN_SINGLE_LAUNCH plans (BASELINE config 2's "single-kernel" form) get the second plan too:
 // their batch-1 transforms are then ONE launch of the two passes (k_fused2b; in place k_fused2bi),
@@ -1898,8 +2034,13 @@ static void make_wide_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, 
   size_t free_b = 0, total_b = 0;
   const bool room = hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b >= kWideMinFreeBytes;
   if (room) {
+#if NTT_DEBUG_CHECKS
     const char* tf = getenv("NTT_TEST_WIDE_FAIL");
-    if (tf && tf[0] == '1') {
+    const bool refuse = tf && tf[0] == '1';
+#else
+    constexpr bool refuse = false;
+#endif
+    if (refuse) {
       void* p = nullptr;
       if (hipMalloc(&p, ~(size_t)0 >> 4) == hipSuccess) (void)hipFree(p);  // refused: the sticky error
     } else {
@@ -2115,7 +2256,34 @@ static int set_profiling(PlanBase& P, int enable) {
   }
   P.profiling = enable != 0;
   P.nrec = 0;
+  P.ev_used = 0;
   return NTT_OK;
+}
+
+// Group mode (PlanBase::begin): the next transform on the plan starts a new slot, the later ones
+// continue it until the next call.
+int ntt_plan_profile_group(ntt_plan* plan) {
+  if (!plan || !plan->impl) return set_err(NTT_ERR_ARG);
+  for (PlanBase* P : {plan->impl.get(), plan->wide.get()})
+    if (P) P->grouped = P->group_new = true;
+  return set_err(NTT_OK);
+}
+
+// Labels of the launches of the latest recorded transform (or group), comma-separated, in launch
+// order: the same intervals as ntt_plan_last_launch_ms.
+int ntt_plan_last_launch_labels(ntt_plan* plan, char* buf, unsigned cap) {
+  if (!plan || !plan->impl || !buf || cap == 0) return set_err(NTT_ERR_ARG);
+  PlanBase& P = plan->last ? *plan->last : *plan->impl;
+  std::string out;
+  for (unsigned i = 1; i < P.ev_used && P.nrec; ++i) {
+    const char* l = P.lab[P.slot][i];
+    if (l[0] == '-' && l[1] == 0) continue;
+    if (!out.empty()) out += ',';
+    out += l;
+  }
+  if (out.size() + 1 > cap) return set_err(NTT_ERR_ARG);
+  memcpy(buf, out.c_str(), out.size() + 1);
+  return set_err(NTT_OK);
 }
 
 int ntt_plan_set_profiling(ntt_plan* plan, int enable) {
@@ -2130,19 +2298,27 @@ int ntt_plan_set_profiling(ntt_plan* plan, int enable) {
 int ntt_plan_last_launch_ms(ntt_plan* plan, float* ms, unsigned max_launches, unsigned* nlaunches) {
   if (!plan || !plan->impl || !ms) return set_err(NTT_ERR_ARG);
   PlanBase& P = plan->last ? *plan->last : *plan->impl;  // the plan that ran the latest transform
-  const unsigned k = P.ev_used ? P.ev_used - 1 : 0;
-  if (nlaunches) *nlaunches = k;
-  if (k == 0 || P.nrec == 0) return set_err(NTT_OK);
+  const unsigned k = P.ev_used ? P.ev_used - 1 : 0;  // intervals of the latest slot (gaps included)
+  auto gap = [&](unsigned i) {
+    const char* l = P.lab[P.slot][i + 1];
+    return l[0] == '-' && l[1] == 0;
+  };
+  unsigned nl = 0;
+  for (unsigned i = 0; i < k; ++i) nl += gap(i) ? 0u : 1u;
+  if (nlaunches) *nlaunches = P.nrec ? nl : 0u;
+  if (nl == 0 || P.nrec == 0) return set_err(NTT_OK);
   if (hipEventSynchronize(P.ev[P.slot][k]) != hipSuccess) return set_err(NTT_ERR_HIP);
   const unsigned nslots = P.nrec < PlanBase::kSlots ? P.nrec : PlanBase::kSlots;
-  for (unsigned i = 0; i < k && i < max_launches; ++i) {
+  unsigned j = 0;
+  for (unsigned i = 0; i < k && j < max_launches; ++i) {
+    if (gap(i)) continue;
     double acc = 0;
     for (unsigned sl = 0; sl < nslots; ++sl) {
       float t = 0;
       if (hipEventElapsedTime(&t, P.ev[sl][i], P.ev[sl][i + 1]) != hipSuccess) return set_err(NTT_ERR_HIP);
       acc += t;
     }
-    ms[i] = (float)(acc / nslots);
+    ms[j++] = (float)(acc / nslots);
   }
   return set_err(NTT_OK);
 }

@@ -173,7 +173,9 @@ int ntt_rplan_create(ntt_rplan** out, int field_id, unsigned log_n, unsigned lim
   }
   if (rc == NTT_OK) {
     const uint64_t g = (uint64_t)rank;
-    rp->rows_no_scale = plan_passes_for(rp->tw, rp->log_n2) == 1;
+    // single-pass row transforms leave n2^-1 to the inverse epilogue table: ask the rows plan itself
+    // which schedule it runs, not the twiddle plan
+    rp->rows_no_scale = plan_passes_for(rp->rows, rp->log_n2) == 1;
     rc = plan_build_fs_table(rp->tw, rp->tab_fwd, rp->log_r, rp->log_n2, g << rp->log_r, 0, false, nullptr);
     if (rc == NTT_OK)
       rc = plan_build_fs_table(rp->tw, rp->tab_inv, rp->log_n1, rp->log_c, 0, g << rp->log_c, true, nullptr,
@@ -373,6 +375,17 @@ int ntt_rplan_set_profiling(ntt_rplan* rp, int enable) {
 int ntt_rplan_last_launch_ms(ntt_rplan* rp, int which, float* ms, unsigned max_launches, unsigned* nlaunches) {
   if (!rp || (which != 0 && which != 1)) return NTT_ERR_ARG;
   return ntt_plan_last_launch_ms(which ? rp->cols : rp->rows, ms, max_launches, nlaunches);
+}
+
+int ntt_rplan_last_launch_labels(ntt_rplan* rp, int which, char* buf, unsigned cap) {
+  if (!rp || (which != 0 && which != 1)) return NTT_ERR_ARG;
+  return ntt_plan_last_launch_labels(which ? rp->cols : rp->rows, buf, cap);
+}
+
+int ntt_rplan_profile_group(ntt_rplan* rp) {
+  if (!rp) return NTT_ERR_ARG;
+  int rc = ntt_plan_profile_group(rp->rows);
+  return rc ? rc : ntt_plan_profile_group(rp->cols);
 }
 
 int ntt_rplan_destroy(ntt_rplan* rp) {

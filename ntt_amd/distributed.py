@@ -340,6 +340,16 @@ class RankPlan:
                       "ntt_rplan_last_launch_ms")
         return [buf[i] for i in range(k.value)]
 
+    def last_launch_labels(self, which: int) -> List[str]:
+        buf = C.create_string_buffer(256)
+        self._L.check(self.lib.ntt_rplan_last_launch_labels(self.handle, which, buf, 256),
+                      "ntt_rplan_last_launch_labels")
+        v = buf.value.decode()
+        return v.split(",") if v else []
+
+    def profile_group(self) -> None:
+        self._L.check(self.lib.ntt_rplan_profile_group(self.handle), "ntt_rplan_profile_group")
+
 
 class DistNTT:
     """One rank of a distributed NTT: the fused rank plan + torch.distributed all-to-all (RCCL on GPUs).
@@ -496,14 +506,19 @@ class DistNTT:
         """This rank's row-layout share of the global synthetic vector (same values as NTTPlan.fill)."""
         return self.engine.fill(t, kind, seed)
 
+    # every call is one timing group of the rank plan (ntt_rplan_profile_group): last_launch_ms then
+    # reports each launch of the call, e.g. the two 2^15-row launches of the row transform at world size 1
     def forward(self, t: torch.Tensor) -> torch.Tensor:
+        self.engine.profile_group()
         return self.fs.forward(t)
 
     def inverse(self, t: torch.Tensor) -> torch.Tensor:
+        self.engine.profile_group()
         return self.fs.inverse(t)
 
     def polymul(self, a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
         """Row-layout shares a, b -> row-layout share of c = a * b (cyclic, length n); two all-to-alls."""
+        self.engine.profile_group()
         return self.fs.polymul(a, b, out)
 
     def set_profiling(self, enable: bool = True) -> None:
@@ -520,8 +535,13 @@ class DistNTT:
             self._x_windows = None
 
     def last_launch_ms(self) -> List[float]:
-        """Row-transform launches, then column-transform launches (separate timing rings)."""
+        """Row-transform launches, then column-transform launches (separate timing rings), of the
+        latest call."""
         return self.engine.last_launch_ms(0) + self.engine.last_launch_ms(1)
+
+    def last_launch_labels(self) -> List[str]:
+        """The same launches' labels (ntt.h ntt_plan_last_launch_labels)."""
+        return self.engine.last_launch_labels(0) + self.engine.last_launch_labels(1)
 
 
 class _RankList:

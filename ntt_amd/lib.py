@@ -47,6 +47,8 @@ PROTOTYPES = {
     "ntt_plan_destroy": (C.c_int, [_vp]),
     "ntt_plan_set_profiling": (C.c_int, [_vp, C.c_int]),
     "ntt_plan_last_launch_ms": (C.c_int, [_vp, C.POINTER(C.c_float), C.c_uint, C.POINTER(C.c_uint)]),
+    "ntt_plan_last_launch_labels": (C.c_int, [_vp, C.c_char_p, C.c_uint]),
+    "ntt_plan_profile_group": (C.c_int, [_vp]),
     "ntt_strerror": (C.c_char_p, [C.c_int]),
     "SSIP": (None, [_vp, C.c_longlong, C.c_uint]),
     "NTT_GZKP_256": (C.c_int, [_vp, C.c_uint32, _vp, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
@@ -92,6 +94,8 @@ PROTOTYPES = {
     "ntt_rplan_fill": (C.c_int, [_vp, _vp, C.c_int, C.c_uint64, _vp]),
     "ntt_rplan_set_profiling": (C.c_int, [_vp, C.c_int]),
     "ntt_rplan_last_launch_ms": (C.c_int, [_vp, C.c_int, C.POINTER(C.c_float), C.c_uint, C.POINTER(C.c_uint)]),
+    "ntt_rplan_last_launch_labels": (C.c_int, [_vp, C.c_int, C.c_char_p, C.c_uint]),
+    "ntt_rplan_profile_group": (C.c_int, [_vp]),
     "ntt_rplan_destroy": (C.c_int, [_vp]),
 }
 

@@ -279,6 +279,17 @@ class NTTPlan:
         _L.check(self._lib.ntt_plan_last_launch_ms(self._h, buf, 16, C.byref(k)), "ntt_plan_last_launch_ms")
         return [buf[i] for i in range(k.value)]
 
+    def last_launch_labels(self) -> List[str]:
+        """Labels of the same launches (ntt.h ntt_plan_last_launch_labels: c8, c8s, f8, ...)."""
+        buf = C.create_string_buffer(256)
+        _L.check(self._lib.ntt_plan_last_launch_labels(self._h, buf, 256), "ntt_plan_last_launch_labels")
+        v = buf.value.decode()
+        return v.split(",") if v else []
+
+    def profile_group(self) -> None:
+        """Group mode (ntt.h ntt_plan_profile_group): later transforms join one record until the next call."""
+        _L.check(self._lib.ntt_plan_profile_group(self._h), "ntt_plan_profile_group")
+
     def close(self) -> None:
         if getattr(self, "_h", None):
             self._lib.ntt_plan_destroy(self._h)

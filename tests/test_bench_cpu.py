@@ -74,3 +74,35 @@ def test_cpu_baseline_fields():
     assert cb["value"] > 0 and cb["unit"] == "field-elements/s" and cb["kind"] == "port"
     assert cb["cores"] >= 1 and isinstance(cb["cpu_model"], str) and cb["cpu_model"]
     assert cb["single_core"]["cores"] == 1 and cb["reference_field_single_core"]["cores"] == 1
+
+
+def test_traffic_pairs_by_launch_label():
+    """PMC bytes attach to this run's launches only when the summary's launches
+    are the same kernels in the same order (labels from tools/pmc_to_traffic.py vs the plan's
+    ntt_plan_last_launch_labels), one timing per launch; else no traffic."""
+    ent = {"launch_bytes": [0.806e9, 0.806e9, 1.25e9, 1.147e9], "launch_labels": ["r8", "r8", "c8", "c8s"]}
+    ok, why = bench.pair_traffic(ent, ["r8", "r8", "c8", "c8s"], [0.30, 0.30, 0.55, 0.47])
+    assert ok == ent["launch_bytes"] and why is None
+    # round 5's world-1 four-step: one row launch missing from the timings -> refused, not shifted
+    bad, why = bench.pair_traffic(ent, ["r8", "c8", "c8s"], [0.316, 0.583, 0.490])
+    assert bad is None and "not this run's launches" in why
+    bad, why = bench.pair_traffic(ent, ["r8", "r8", "c8", "c8s"], [0.30, 0.55, 0.47])
+    assert bad is None
+    bad, why = bench.pair_traffic({"launch_bytes": [1.0, 2.0]}, ["c8", "f8"], [0.5, 0.4])
+    assert bad is None and "without per-launch labels" in why
+    bad, why = bench.pair_traffic(None, ["c8"], [0.5])
+    assert bad is None
+
+
+def test_pmc_labels_from_kernel_names():
+    """tools/pmc_to_traffic.py names launches as the plan does (include/ntt.h ntt_plan_last_launch_labels)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from pmc_to_traffic import launch_label
+    E = "ntt::Eng29<9, 8, 0, 0>"
+    assert launch_label(f"void ntt::k_pass<{E}, 8, 0, true, true, 0, true, 0, false>(unsigned int const*)") == "c8"
+    assert launch_label(f"void ntt::k_pass<{E}, 8, 0, true, true, 0, true, 0, true>(unsigned int const*)") == "c8s"
+    assert launch_label(f"void ntt::k_pass<{E}, 8, 1, false, true, 0, true, 0, false>(x)") == "f8"
+    assert launch_label("void ntt::k_pass<ntt::Eng32<1, 2, 0>, 6, 5, false, true, 0, true, 2, false>(x)") == "r6"
+    assert launch_label(f"void ntt::k_final_ipn<{E}, 8>(unsigned int*)") == "i8"
+    assert launch_label("void ntt::k_fused2b<ntt::Eng29<9, 8, 0, 12>, 10, 10>(x)") == "b"
+    assert launch_label("void ntt::k_build_tw<ntt::Eng29<9, 8, 0, 0> >(x)") == ""

@@ -127,6 +127,18 @@ def test_dist_ntt_rccl_world1():
             assert torch.equal(t, x[_index(d.layout, "col")]), pieces
             d.inverse(t)
             assert torch.equal(t, t0), pieces
+        # the per-launch timings of one call report EVERY launch, with its label.
+        # At 2^24 (16 + 8) the row transform runs as two launches of 2^15 rows, then the column
+        # transforms' two passes: four launches, the first two of one kind.
+        d = DistNTT(1, 24, 4, device=0)
+        t = d.fill(d.empty(), "random", seed=2)
+        d.set_profiling(True)
+        for _ in range(3):
+            d.forward(t)
+        ms, labels = d.last_launch_ms(), d.last_launch_labels()
+        d.set_profiling(False)
+        assert len(ms) == 4 and len(labels) == 4, (ms, labels)
+        assert labels[0] == labels[1] and all(labels) and all(m > 0 for m in ms), (ms, labels)
     finally:
         dist.destroy_process_group()
 

@@ -1,6 +1,7 @@
 """BASELINE config 2 as a single kernel (VERDICT r02 missing 1): NTT_PLAN_SINGLE_LAUNCH runs a 3-pass
 transform as ONE persistent launch, in both forms (NTT_FUSED_MODE, read when a plan builds its fused
-schedule): "1" two grid barriers over a cooperative launch (k_fused3b, the default), "0" the passes'
+schedule): "1" two grid barriers (k_fused3b, the default; a plain launch since round 5, the cooperative
+launch retired in round 6), "0" the passes'
 tiles handed between workgroups through dependency counters (k_fused3).  Checked bit for bit against the threaded C oracle (GZKP-NTT.cu:30-48, inverse
 GZKP-NTT.cu:1725-1732) at C2's 2^20 on vectors A (x_j = j, the reference's input) and B, against the
 default 3-launch schedule at every fused size 2^18..2^24 for BN254 and BLS12-381 (4 limbs), over
@@ -190,16 +191,14 @@ print("plain-launch ok")
 """
 
 
-@pytest.mark.parametrize("env", [{"NTT_FUSED_COOP": "1", "NTT_FUSED_MODE": "1"},
-                                 {"NTT_WIDE_TILES": "0", "NTT_FUSED_MODE": "1"},
+@pytest.mark.parametrize("env", [{"NTT_WIDE_TILES": "0", "NTT_FUSED_MODE": "1"},
                                  {"NTT_WIDE_TILES": "0", "NTT_FUSED_MODE": "0"}],
-                         ids=["cooperative_launch", "three_pass_2pow20_barriers", "three_pass_2pow20_dataflow"])
+                         ids=["three_pass_2pow20_barriers", "three_pass_2pow20_dataflow"])
 def test_grid_barrier_forms_in_child_processes(env):
-    """Environment switches are read once per process, so in a child process: NTT_FUSED_COOP=1, the
-    grid-barrier single launches (default and in place) as cooperative launches (round 5: plain
-    launches are the default); NTT_WIDE_TILES=0, the
+    """Environment switches are read once per process, so in a child process: NTT_WIDE_TILES=0, the
     1024-element-tile single launches at 2^20 too (k_fused3b / k_fused3 / k_fused3bi, as before round
-    5).  Each gives the default schedule's results."""
+    5).  Each gives the default schedule's results.  (Round 6 retired the cooperative-launch switch,
+    NTT_FUSED_COOP: VERDICT r05 item 5.)"""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -213,10 +213,14 @@ print("child ok")
 def test_failed_second_plan_leaves_no_error_behind(tmp_path):
     """when the 4096-element-tile plan cannot be built (its allocation refused),
     the plan runs alone on 1024-element tiles and its first forward returns NTT_OK with the same
-    output as a plan that has the second plan (the refused allocation's sticky error is cleared)."""
+    output as a plan that has the second plan (the refused allocation's sticky error is cleared).
+    The refusal hook exists in the checked build only: the child loads libntt_debug.so."""
     from ntt_amd.ntt import NTTPlan
+    dbg = os.path.join(ROOT, "ntt_amd", "libntt_debug.so")
+    if not os.path.exists(dbg):
+        pytest.skip("checked build not built (python -m ntt_amd.build --debug)")
     path = str(tmp_path / "fail.npy")
-    env = dict(os.environ, NTT_TEST_WIDE_FAIL="1")
+    env = dict(os.environ, NTT_TEST_WIDE_FAIL="1", NTT_LIB_PATH=dbg)
     r = subprocess.run([sys.executable, "-c", _CHILD_FAIL.format(root=ROOT, path=path)], env=env,
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "child ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
@@ -225,3 +229,44 @@ def test_failed_second_plan_leaves_no_error_behind(tmp_path):
     t = pl.fill(pl.empty(), "random", seed=51)
     pl.forward(t)
     assert np.array_equal(t.cpu().numpy(), np.load(path))
+
+
+_CHILD_NO_HOOK = r"""
+import sys
+sys.path.insert(0, {root!r})
+from ntt_amd.ntt import NTTPlan
+assert NTTPlan(1, 20, 4).passes == [10, 10]
+print("child ok")
+"""
+
+
+def test_product_build_has_no_failure_hook():
+    """NTT_TEST_WIDE_FAIL is read by the checked build only; the product library
+    builds its second plan regardless."""
+    env = dict(os.environ, NTT_TEST_WIDE_FAIL="1")
+    env.pop("NTT_LIB_PATH", None)
+    r = subprocess.run([sys.executable, "-c", _CHILD_NO_HOOK.format(root=ROOT)], env=env, capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0 and "child ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_launch_labels_name_the_schedule():
+    """ntt_plan_last_launch_labels (round 6): the kinds and radices of the latest transform's launches,
+    the names bench.py pairs PMC bytes by (tools/pmc_to_traffic.py derives them from kernel names)."""
+    from ntt_amd.ntt import NTTPlan
+    for fid, log_n, kw, want in [(1, 24, {}, ["c8", "c8s", "f8"]), (1, 20, {}, ["c10", "f10"]),
+                                 (1, 20, {"single_launch": True}, ["b"]), (1, 8, {}, ["s8"])]:
+        pl = NTTPlan(fid, log_n, 4, **kw)
+        t = pl.fill(pl.empty(), "random", seed=9)
+        pl.set_profiling(True)
+        pl.forward(t)
+        assert pl.last_launch_labels() == want, (log_n, kw, pl.last_launch_labels())
+        assert len(pl.last_launch_ms()) == len(want)
+        pl.set_profiling(False)
+    pl = NTTPlan(1, 20, 4)
+    b = pl.empty(2)
+    pl.fill(b.view(2, pl.n, -1)[0], "random", seed=1)
+    pl.set_profiling(True)
+    pl.forward_batch(b, 2)  # batched: the 1024-element tiles, 7 + 7 + 6
+    assert pl.last_launch_labels() == ["c7", "c7s", "f6"], pl.last_launch_labels()
+    pl.set_profiling(False)

@@ -10,6 +10,7 @@ builds for the plain C++ form).
 
     python tools/gen_field29_asm.py > ntt_amd/csrc/field29_asm9.hpp
 """
+import sys
 L = 9
 
 
@@ -260,42 +261,44 @@ def gen_mont_whole():
 
 
 def main():
-    print("// GENERATED by tools/gen_field29_asm.py -- do not edit.")
+    # The checked-in header (ntt_amd/csrc/field29_asm9.hpp) holds the product form only.  The measured
+    # alternatives stay here as generator options, for experiment builds:
+    #   --whole  one asm statement per product (1.73 vs 1.67 ms at 2^24 BN254: spills, no ILP across products)
+    #   --pair   two product columns per statement, their MAD chains interleaved (+2.0 %)
+    variant = "whole" if "--whole" in sys.argv else ("pair" if "--pair" in sys.argv else "")
+    print("// GENERATED by tools/gen_field29_asm.py" + (f" --{variant}" if variant else "") + " -- do not edit.")
     print("// L = 9 radix-2^29 products (field29.hpp mulc29 / mont29) with one inline-asm MAD chain per")
     print("// product column; see the generator for why.  Device only.")
     print("#pragma once")
     print('#include "field29.hpp"')
     print()
     print("namespace ntt {")
-    print("#ifndef NTT_ASM_WHOLE")
-    print("#define NTT_ASM_WHOLE 0  // measured slower: 1.73 vs 1.67 ms (2^24 BN254; spills, no ILP across products)")
-    print("#endif")
-    print("#ifndef NTT_MULC_PAIR")
-    print("#define NTT_MULC_PAIR 0")
-    print("#endif")
-    print("#if defined(__HIP_DEVICE_COMPILE__) && NTT_ASM_WHOLE")
-    print("// one asm statement per product (see the generator)")
-    print(gen_mulc_whole())
-    print()
-    print(gen_mont_whole())
-    print("__device__ __forceinline__ void mulc29_a9u(uint32_t (&r)[9], const uint32_t (&x)[9], const uint32_t (&w)[9],")
-    print("                                           const uint32_t (&ws)[9], const uint32_t (&pbar)[9]) {")
-    print("  mulc29_a9(r, x, w, ws, pbar);")
-    print("}")
-    print("#elif defined(__HIP_DEVICE_COMPILE__) && NTT_MULC_PAIR")
-    print("// two product columns per asm statement, their MAD chains interleaved (see the generator)")
-    print(gen_mulc_pair())
-    print()
-    print(gen_mulc_pair(uniform=True))
-    print()
-    print(gen_mont())
-    print("#elif defined(__HIP_DEVICE_COMPILE__)")
-    print("// one asm statement per product column")
-    print(gen_mulc())
-    print()
-    print(gen_mulc(uniform=True))
-    print()
-    print(gen_mont())
+    if variant == "whole":
+        print("#if defined(__HIP_DEVICE_COMPILE__)")
+        print("// one asm statement per product (see the generator)")
+        print(gen_mulc_whole())
+        print()
+        print(gen_mont_whole())
+        print("__device__ __forceinline__ void mulc29_a9u(uint32_t (&r)[9], const uint32_t (&x)[9], const uint32_t (&w)[9],")
+        print("                                           const uint32_t (&ws)[9], const uint32_t (&pbar)[9]) {")
+        print("  mulc29_a9(r, x, w, ws, pbar);")
+        print("}")
+    elif variant == "pair":
+        print("#if defined(__HIP_DEVICE_COMPILE__)")
+        print("// two product columns per asm statement, their MAD chains interleaved (see the generator)")
+        print(gen_mulc_pair())
+        print()
+        print(gen_mulc_pair(uniform=True))
+        print()
+        print(gen_mont())
+    else:
+        print("#if defined(__HIP_DEVICE_COMPILE__)")
+        print("// one asm statement per product column")
+        print(gen_mulc())
+        print()
+        print(gen_mulc(uniform=True))
+        print()
+        print(gen_mont())
     print("#else  // host pass: the generic forms (same results)")
     print("F29_HD void mulc29_a9(uint32_t (&r)[9], const uint32_t (&x)[9], const uint32_t (&w)[9], const uint32_t (&ws)[9],")
     print("                       const uint32_t (&pbar)[9]) {")

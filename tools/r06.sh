@@ -38,7 +38,16 @@ for s in $ARGS; do
         step pmc_${v}_write 120 env $E rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc_$v/write -o run --output-format csv -- python3 bench.py $BQ
         step pmc_${v}_l2 120 env $E rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum -d $O/pmc_$v/l2 -o run --output-format csv -- python3 bench.py $BQ
       done ;;
-    new) step pytest_new 900 $PYT tests/test_gpu_wide_tiles.py tests/test_gpu_single_launch.py tests/test_gpu_watchdog.py ;;
+    new) step pytest_new 900 $PYT tests/test_gpu_fused_order.py tests/test_gpu_wide_tiles.py tests/test_gpu_single_launch.py tests/test_gpu_watchdog.py ;;
+    dist1) step pytest_dist1 600 $PYT tests/test_gpu_distributed.py -k "rccl_world1" ;;
+    trace) step fused_trace 300 python3 -u tools/exp_fused_trace.py --calls 60 --out $O/fused_trace.jsonl ;;
+    c2) # the C2 forms, two interleaved repetitions, fresh process each: the library's single-launch
+      # ordering on (default) and off (NTT_FUSED_ORDER=0)
+      C2="--cfg f1_L4_n20 --cfg f1_L4_n20_sl --cfg f1_L4_n20_ip_sl --cfg f1_L4_n19_sl --cfg f1_L4_n19_ip_sl"
+      for i in ${C2_REPS:-1 2}; do
+        step c2_order_$i 200 python3 -u tools/exp_launches.py $C2 --warmup 50 --steps 200 --out $O/c2_order_$i.jsonl
+        step c2_noorder_$i 200 env NTT_FUSED_ORDER=0 python3 -u tools/exp_launches.py $C2 --warmup 50 --steps 200 --out $O/c2_noorder_$i.jsonl
+      done ;;
     tests) step pytest_gpu 1100 $PYT tests -m gpu ;;
     dbg) step pytest_dbg 600 $PYT tests/test_gpu_debug_build.py ;;
     smoke) step smoke 120 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
