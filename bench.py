@@ -148,7 +148,45 @@ def cpu_baseline(field_id: int, limbs: int, log_n: int):
     OC.ntt_mp_par(xb, p, g, threads)
     dtp = time.perf_counter() - t0
     cpu = _cpu_model()
+    # SURVEY §8(d)'s per-config CPU runs: C1 and 2^20 in full, 2^24 once (above), 2^28 extrapolated
+    # from the 2^24 run by n log n and labelled so (the reference's own CPU timings for comparison:
+    # self-sort-in-place.cu:450-471, GZKP-NTT.cu:1592-1599)
+    from ntt_amd import plumbing
+    t0 = time.perf_counter()
+    plumbing.cpu_ntt_c1(12)
+    dc1 = time.perf_counter() - t0
+    x = OC.random_limbs(field_id, 1 << 12, seed=1, L=limbs)
+    t0 = time.perf_counter()
+    OC.ntt_mp(x, p, g)
+    dc1c = time.perf_counter() - t0
+    x = OC.random_limbs(field_id, 1 << 20, seed=2, L=limbs)
+    t0 = time.perf_counter()
+    OC.ntt_mp_par(x, p, g, threads)
+    d20p = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    OC.ntt_mp(x, p, g)
+    d20 = time.perf_counter() - t0
+    del x
+    t28 = dtp * (1 << (28 - big)) * 28 / big
+    configs = {
+        "C1_2^12_python": {"value": 4096 / dc1, "seconds": dc1, "cores": 1, "kind": "port",
+                           "sample": "C1: 2^12-point forward NTT of x_j = j over BN254 Fr by the repo's Python CPU "
+                                     "path (ntt_amd/plumbing.cpu_ntt_c1: radix-2 DIF + bit reversal), in full"},
+        "C1_2^12_c": {"value": 4096 / dc1c, "seconds": dc1c, "cores": 1, "kind": "port",
+                      "sample": f"2^12-point forward NTT ({FIELD_NAMES[field_id]}, SplitMix64 seed 1), scalar C "
+                                "oracle, in full"},
+        "2^20": {"value": (1 << 20) / d20p, "seconds": d20p, "cores": threads, "kind": "port",
+                 "single_core": {"value": (1 << 20) / d20, "seconds": d20, "cores": 1},
+                 "sample": f"2^20-point forward NTT ({FIELD_NAMES[field_id]}, seed 2), C oracle over {threads} "
+                           "OpenMP threads and on 1 core, in full"},
+        "2^24": {"value": (1 << big) / dtp, "seconds": dtp, "cores": threads, "kind": "port",
+                 "sample": "the headline cpu_baseline run above, once"},
+        "2^28_extrapolated": {"value": (1 << 28) / t28, "seconds": t28, "cores": threads, "kind": "port",
+                              "extrapolated": True,
+                              "sample": "EXTRAPOLATED, not run: the 2^24 run's time x 16 x 28/24 (n log2 n)"},
+    }
     return {"value": (1 << big) / dtp, "unit": "field-elements/s", "cores": threads, "kind": "port",
+            "configs": configs,
             "cpu_model": cpu,
             "sample": f"one 2^{big}-point forward NTT ({FIELD_NAMES[field_id]}, {limbs}x64-bit limbs, SplitMix64 "
                       f"input) by the C oracle split over {threads} OpenMP threads ({cpu}): {dtp:.2f} s",
@@ -221,11 +259,17 @@ def visible_devices() -> int:
     before the launcher" must not rest on what device_count() happens to do on one image)."""
     import subprocess
     code = "import torch; print(torch.cuda.device_count())"
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600)
     try:
+        r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=600)
+    except subprocess.TimeoutExpired:
+        raise SystemExit("bench.py: the device-count probe (a child importing torch) did not finish in 600 s")
+    try:
+        if r.returncode != 0:
+            raise ValueError
         return int(r.stdout.strip().splitlines()[-1])
     except (ValueError, IndexError):
-        return 0
+        # the probe failed (not "0 devices"): say so, with the child's own error
+        raise SystemExit(f"bench.py: the device-count probe failed (exit {r.returncode}):\n{r.stderr[-2000:]}")
 
 
 def spawn_ranks(args) -> int:

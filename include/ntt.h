@@ -114,12 +114,15 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
  * (k_fused3bi).  Same contract and results as the default schedule; batch 1; other plans and calls
  * ignore the flag.
  * The grid-barrier forms are plain launches of at most as many workgroups as the device keeps
- * resident (the plan's occupancy query), so they assume no other persistent kernel holds part of the
- * device meanwhile: two single-launch plans on two streams of one device could each wait for the
- * other's workgroups.  Every wait is bounded: such a call returns garbage and the plan's next call
- * NTT_ERR_DEVICE (ntt_plan_device_status), never a hang.  Environment NTT_FUSED_COOP=1 uses a
- * cooperative launch instead (co-residency guaranteed, ~20 us more per call; under rocprofv3 such
- * processes crashed at exit in round 4).
+ * resident (the plan's occupancy query).  The library orders them per device (round 6): a single
+ * launch enqueued on another stream than the device's previous one waits for it, so two
+ * single-launch plans on two streams never split the device between them (on one stream nothing is
+ * added).  CUs held by anything else (another process, a persistent kernel of the caller's) can still
+ * keep part of a launch waiting; every wait is bounded, so the call then returns garbage and the
+ * plan's next call NTT_ERR_DEVICE (ntt_plan_device_status), never a hang.  The in-place forms
+ * (k_fused2bi, k_fused3bi) check residency before their first store: such a call stores nothing and
+ * the caller's buffer keeps its input.  (The cooperative-launch switch NTT_FUSED_COOP was retired in
+ * round 6.)
  * ntt_plan_device_status reports a wait that gave up (a watchdog; never expected). */
 #define NTT_PLAN_SINGLE_LAUNCH 32u
 /* Rival schedule, the reference's `naive` (GZKP-NTT.cu:59-95, big-num.cu:67-170): the bit reversal,

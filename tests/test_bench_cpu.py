@@ -74,6 +74,13 @@ def test_cpu_baseline_fields():
     assert cb["value"] > 0 and cb["unit"] == "field-elements/s" and cb["kind"] == "port"
     assert cb["cores"] >= 1 and isinstance(cb["cpu_model"], str) and cb["cpu_model"]
     assert cb["single_core"]["cores"] == 1 and cb["reference_field_single_core"]["cores"] == 1
+    # C1 and 2^20 in full, 2^24 once, 2^28 extrapolated and labelled
+    c = cb["configs"]
+    assert set(c) == {"C1_2^12_python", "C1_2^12_c", "2^20", "2^24", "2^28_extrapolated"}
+    assert all(v["value"] > 0 and v["seconds"] > 0 and v["cores"] >= 1 for v in c.values())
+    assert c["2^28_extrapolated"]["extrapolated"] is True and "EXTRAPOLATED" in c["2^28_extrapolated"]["sample"]
+    assert not any(v.get("extrapolated") for k, v in c.items() if k != "2^28_extrapolated")
+    assert c["2^20"]["single_core"]["cores"] == 1
 
 
 def test_traffic_pairs_by_launch_label():
@@ -106,3 +113,12 @@ def test_pmc_labels_from_kernel_names():
     assert launch_label(f"void ntt::k_final_ipn<{E}, 8>(unsigned int*)") == "i8"
     assert launch_label("void ntt::k_fused2b<ntt::Eng29<9, 8, 0, 12>, 10, 10>(x)") == "b"
     assert launch_label("void ntt::k_build_tw<ntt::Eng29<9, 8, 0, 0> >(x)") == ""
+
+
+def test_device_probe_failure_is_reported(monkeypatch):
+    """a failing device-count child is a reported failure, not '0 devices'."""
+    import pytest
+    monkeypatch.setattr(sys, "executable", "/bin/false")
+    with pytest.raises(SystemExit) as ei:
+        bench.visible_devices()
+    assert "probe failed" in str(ei.value)

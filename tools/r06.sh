@@ -40,6 +40,30 @@ for s in $ARGS; do
       done ;;
     new) step pytest_new 900 $PYT tests/test_gpu_fused_order.py tests/test_gpu_wide_tiles.py tests/test_gpu_single_launch.py tests/test_gpu_watchdog.py ;;
     dist1) step pytest_dist1 600 $PYT tests/test_gpu_distributed.py -k "rccl_world1" ;;
+    wt) # timing only: k_fused2b with plain (not write-through) pass-1 stores (libntt_wt.so, results not
+      # guaranteed) against the product, per-phase trace and per-call time, interleaved twice
+      for i in 1 2; do
+        step trace_prod_$i 300 python3 -u tools/exp_fused_trace.py --calls 60 --out $O/trace_prod_$i.jsonl
+        step trace_wt_$i 300 env NTT_LIB_PATH=ntt_amd/libntt_wt.so python3 -u tools/exp_fused_trace.py --calls 60 --out $O/trace_wt_$i.jsonl
+        step c2_prod_$i 200 python3 -u tools/exp_launches.py --cfg f1_L4_n20 --cfg f1_L4_n20_sl --warmup 50 --steps 200 --out $O/c2_prod_$i.jsonl
+        step c2_wt_$i 200 env NTT_LIB_PATH=ntt_amd/libntt_wt.so python3 -u tools/exp_launches.py --cfg f1_L4_n20 --cfg f1_L4_n20_sl --warmup 50 --steps 200 --out $O/c2_wt_$i.jsonl
+      done ;;
+    rel) # timing only: k_fused2b with plain pass-1 stores and one agent-scope release per workgroup before
+      # the barrier (libntt_rel.so) against the product, interleaved twice
+      for i in 1 2; do
+        step trace_prod_$i 300 python3 -u tools/exp_fused_trace.py --calls 60 --out $O/trace_prod_$i.jsonl
+        step trace_rel_$i 300 env NTT_LIB_PATH=ntt_amd/libntt_rel.so python3 -u tools/exp_fused_trace.py --calls 60 --out $O/trace_rel_$i.jsonl
+        step c2_prod_$i 200 python3 -u tools/exp_launches.py --cfg f1_L4_n20 --cfg f1_L4_n20_sl --warmup 50 --steps 200 --out $O/c2_prod_$i.jsonl
+        step c2_rel_$i 200 env NTT_LIB_PATH=ntt_amd/libntt_rel.so python3 -u tools/exp_launches.py --cfg f1_L4_n20 --cfg f1_L4_n20_sl --warmup 50 --steps 200 --out $O/c2_rel_$i.jsonl
+      done
+      step rel_parity 300 env NTT_LIB_PATH=ntt_amd/libntt_rel.so python3 -u -c "
+import sys, torch; sys.path.insert(0, '.')
+from ntt_amd.ntt import NTTPlan
+a = NTTPlan(1, 20, 4, single_launch=True); r = NTTPlan(1, 20, 4)
+bad = 0
+for s in range(20):
+    x = a.fill(a.empty(), 'random', seed=s); y = x.clone(); a.forward(x); r.forward(y); bad += int(not torch.equal(x, y))
+print('mismatches', bad, 'of 20')" ;;
     trace) step fused_trace 300 python3 -u tools/exp_fused_trace.py --calls 60 --out $O/fused_trace.jsonl ;;
     c2) # the C2 forms, two interleaved repetitions, fresh process each: the library's single-launch
       # ordering on (default) and off (NTT_FUSED_ORDER=0)
