@@ -80,6 +80,12 @@ print('mismatches', bad, 'of 20')" ;;
     fs1) step bench_fourstep_w1 300 python3 -u bench.py --four-step --steps 20 --warmup 10 --no-cpu-baseline ;;
     prof) step rocprof_stats 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py ;;
     configs) step configs 900 python3 -u tools/bench_configs.py --out $O/configs.jsonl ;;
+    pmc_rl) step pmc_ranklocal 900 env O=$O/pmc_rl WORLDS="1 2 4 8" bash tools/pmc_ranklocal.sh ;;
+    reh2) step bench_n2_rehearsal 400 env NTT_BENCH_EXCHANGE=host python3 -u bench.py --gpus 2 --steps 20 --warmup 10 ;;
+    reh4) step bench_n4_rehearsal 600 env NTT_BENCH_EXCHANGE=host python3 -u bench.py --gpus 4 --steps 10 --warmup 5 ;;
+    reh8) step bench_n8_rehearsal 600 env NTT_BENCH_EXCHANGE=host python3 -u bench.py --gpus 8 --steps 10 --warmup 5 ;;
+    rl28) step ranklocal_c4 300 python3 -u tools/exp_ranklocal.py --log-n 28 --worlds 8 --warmup 5 --steps 10 --out $O/ranklocal_c4.jsonl ;;
+    stress) step stress 1000 python3 -u tools/stress_sync.py --reps ${STRESS_REPS:-400} --out $O/stress.jsonl ;;
     pmc)
       step pmc_sq 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE -d $O/pmc/sq -o run --output-format csv -- python3 bench.py $BQ
       step pmc_fetch 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O/pmc/fetch -o run --output-format csv -- python3 bench.py $BQ
