@@ -140,6 +140,31 @@ int ntt_plan_create(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs
  * 4-limb plans; the plan's other calls run the default schedule.  Exclusive with the other rivals and
  * with NTT_PLAN_IN_PLACE. */
 #define NTT_PLAN_NO_SWAP 128u
+/* Rival schedules, the reference's bealto.com radix-2^deg Stockham family (round 6): log2 n / deg
+ * rounds of one launch each, ping-pong between the caller's buffer and a plan buffer, natural order
+ * in and out.  A group of 2^deg elements x[index + i t] (t = n / 2^deg) is multiplied by
+ * w^((n >> lgp >> deg) k i) (k = index mod 2^lgp), transformed by deg radix-2 rounds in LDS with the
+ * 2^(max_deg-1)-entry table pq, and written to y[((index - k) << deg) + k + i 2^lgp]; two elements per
+ * thread.  The variants differ only in how threads, groups and LDS rows map (the reference's access
+ * patterns, kept for comparison):
+ *   NTT_PLAN_BELLPERSON   bellperson_baseline / FIELD_radix_fft_revised (GZKP-NTT.cu:391-553): one
+ *                         group per workgroup, deg <= 8, inputs bit-reversed into LDS, DIT rounds;
+ *   NTT_PLAN_IMPROVED_V1  improve_grouped (GZKP-NTT.cu:556-630, 721-804): 32 groups per workgroup,
+ *                         deg <= 3, DIF rounds, outputs bit-reversed from LDS;
+ *   NTT_PLAN_IMPROVED_V2  improve_group_coalesced_read (632-719, 806-890): v1 with the load map
+ *                         transposed, consecutive threads reading consecutive groups;
+ *   NTT_PLAN_IMPROVED_V3  improve_group_coalesced_read_and_write (892-1075): v2 with the stores on
+ *                         the load map too (after the first round);
+ *   NTT_PLAN_IMPROVED_V4  improve_reduce_bank_conflict (1077-1296): v3 with each group's LDS row
+ *                         padded by one element.
+ * The reference runs them on P469762049 (`long long`); here forward single transforms of P469762049
+ * and 4-limb plans, the plan's other calls on the default schedule.  Exclusive with the other rivals
+ * and with NTT_PLAN_IN_PLACE. */
+#define NTT_PLAN_BELLPERSON 256u
+#define NTT_PLAN_IMPROVED_V1 512u
+#define NTT_PLAN_IMPROVED_V2 1024u
+#define NTT_PLAN_IMPROVED_V3 2048u
+#define NTT_PLAN_IMPROVED_V4 4096u
 int ntt_plan_create_ex(ntt_plan** out, int field_id, unsigned log_n, unsigned limbs64, int device, unsigned flags);
 /* Device-side status of a plan (blocking: synchronises the device, then reads and clears it).
  * *bad bit 0: an inter-workgroup wait gave up at its watchdog (NTT_PLAN_SINGLE_LAUNCH, or the fused

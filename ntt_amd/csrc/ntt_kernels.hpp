@@ -246,6 +246,17 @@ hipError_t launch_build_pow(uint32_t* out, size_t count, const uint32_t* lo, con
 template <class E>
 hipError_t launch_noswap_round(const uint32_t* src, uint32_t* dst, uint32_t log_n, uint32_t log_s, const uint32_t* pw,
                                const typename E::Args& F, hipStream_t st);
+// The reference's bealto.com radix-2^deg Stockham family (ntt.h NTT_PLAN_BELLPERSON,
+// NTT_PLAN_IMPROVED_V1..V4): one round of 2^deg-point groups, 2^log_g groups per workgroup
+// (A: tw_lo / tw_hi / lo_bits two-level tables for the input twiddles, tw_int the pq table of
+// w_{2^max_deg}^j Shoup pairs, j < 2^(max_deg - 1)).  Engines with HasStockham only.
+enum : int { BEALTO_BELLPERSON = 0, BEALTO_V1 = 1, BEALTO_V2 = 2, BEALTO_V3 = 3, BEALTO_V4 = 4 };
+struct BealtoArgs {
+  uint32_t log_n, lgp, deg, log_g, max_deg;
+};
+template <class E>
+hipError_t launch_bealto(int variant, const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, const BealtoArgs& B,
+                         hipStream_t st);
 template <class E>
 hipError_t launch_naive_round(const uint32_t* src, uint32_t* dst, uint32_t log_n, uint32_t log_s, const uint32_t* pw,
                               const typename E::Args& F, hipStream_t st);

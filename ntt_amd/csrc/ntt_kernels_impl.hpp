@@ -1531,6 +1531,131 @@ hipError_t launch_naive_round(const uint32_t* src, uint32_t* dst, uint32_t log_n
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------- bealto / bellperson rivals
+// The reference's radix-2^deg Stockham family (bealto.com's group FFT as bellperson ships it,
+// FIELD_radix_fft_revised, GZKP-NTT.cu:391-464, and the four "improved" kernels, GZKP-NTT.cu:556-630,
+// 632-719, 892-989, 1077-1210; ntt.h NTT_PLAN_BELLPERSON / NTT_PLAN_IMPROVED_V1..V4) as ONE kernel
+// with the variant as a template argument: they compute the same round and differ only in how
+// threads, groups and LDS rows are mapped, which is what they are kept for (comparison).  A round
+// takes groups `index` of 2^deg elements x[index + i t] (t = n >> deg), multiplies element i by
+// w_n^(e i), e = (n >> lgp >> deg) (index mod 2^lgp) (from the two-level tables: the reference raises
+// FIELD_pow_lookup's twiddle per thread), runs deg radix-2 rounds in LDS with the pq table and writes
+// y[((index - k) << deg) + k + i 2^lgp].  lsize = 2^(deg-1) threads per group, two elements each.
+//   bellperson: inputs land bit-reversed in LDS, DIT rounds (twiddle, then butterfly), natural out;
+//   v1:         DIF rounds (butterfly, then twiddle), bit-reversed out; 2^log_g groups per workgroup;
+//   v2:         loads on the transposed map (thread -> group tid mod G: coalesced x[index + i t]);
+//   v3:         and stores on it too when lgp > 0 (consecutive k: coalesced y);
+//   v4:         and LDS rows of 2 lsize + 1 elements (the reference's bank-conflict padding).
+// Lazy bounds (Eng29): loads < p, input products < 3p, every butterfly's outputs brought back < 4p.
+__device__ __forceinline__ uint32_t brev_rt(uint32_t v, uint32_t bits) {
+  return bits ? __builtin_bitreverse32(v) >> (32u - bits) : 0u;
+}
+template <class E>
+__device__ __forceinline__ void lds_put_el(uint32_t* u, uint32_t slot, const uint32_t (&v)[E::W]) {
+#pragma unroll
+  for (int w = 0; w < E::W; ++w) u[(size_t)slot * E::W + w] = v[w];
+}
+template <class E>
+__device__ __forceinline__ void lds_get_el(uint32_t (&v)[E::W], const uint32_t* u, uint32_t slot) {
+#pragma unroll
+  for (int w = 0; w < E::W; ++w) v[w] = u[(size_t)slot * E::W + w];
+}
+template <class E, int V>
+__global__ __launch_bounds__(1024) void k_bealto(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                 const PassArgs<E> A, const BealtoArgs B) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t u_g[];
+  const uint32_t deg = B.deg, lsz = 1u << (deg - 1), G = 1u << B.log_g, tid = threadIdx.x;
+  const size_t t = (size_t)1 << (B.log_n - deg), p = (size_t)1 << B.lgp;
+  const uint32_t rl = 2 * lsz + (V == BEALTO_V4 ? 1u : 0u);  // one group's LDS row, elements
+  // compute map: group gid, lane lid; load map: transposed from v2 on
+  const uint32_t lid = tid & (lsz - 1), gid = tid >> (deg - 1);
+  const uint32_t gid_r = V >= BEALTO_V2 ? (tid & (G - 1)) : gid, lid_r = V >= BEALTO_V2 ? (tid >> B.log_g) : lid;
+  const size_t index = (size_t)blockIdx.x * G + gid, index_r = (size_t)blockIdx.x * G + gid_r;
+  const size_t k = index & (p - 1), k_r = index_r & (p - 1);
+  {
+    const size_t e = (t >> B.lgp) * k_r;  // w_n^(e i): < n for i < 2^deg
+    uint32_t* u = u_g + (size_t)gid_r * rl * E::W;
+#pragma unroll
+    for (uint32_t j = 0; j < 2; ++j) {
+      const uint32_t i = 2 * lid_r + j;
+      uint32_t v[E::W];
+      E::load(v, src, index_r + i * t);
+      const size_t ei = e * i;
+      typename E::Tw tl, th;
+      E::tload(tl, A.tw_lo, (uint32_t)(ei & ((1u << A.lo_bits) - 1)));
+      E::tload(th, A.tw_hi, (uint32_t)(ei >> A.lo_bits));
+      E::mul(tl.w, th, A.F);  // (lo R_e) hi
+      E::mulv(v, tl.w, A.F);  // v w_n^(e i), < 3p
+      lds_put_el<E>(u, V == BEALTO_BELLPERSON ? brev_rt(i, deg) : i, v);
+    }
+  }
+  __syncthreads();
+  {
+    uint32_t* u = u_g + (size_t)gid * rl * E::W;
+    const uint32_t pqshift = B.max_deg - deg;
+    for (uint32_t s = 0; s < deg; ++s) {
+      const uint32_t rnd = V == BEALTO_BELLPERSON ? deg - 1 - s : s;
+      const uint32_t bit = lsz >> rnd, di = lid & (bit - 1), i0 = (lid << 1) - di, i1 = i0 + bit;
+      uint32_t a[E::W], b[E::W];
+      lds_get_el<E>(a, u, i0);
+      lds_get_el<E>(b, u, i1);
+      typename E::Tw w;
+      if (di) E::tload(w, A.tw_int, di << rnd << pqshift);  // w_{2^(deg - rnd)}^di
+      if constexpr (V == BEALTO_BELLPERSON) {  // DIT: twiddle, then butterfly
+        if (di) E::mul(b, w, A.F);
+        E::template bfly_l<E::IN>(a, b, A.F);
+        E::template reduce<2 * E::IN, E::IN>(b, A.F);
+      } else {  // DIF: butterfly, then twiddle
+        E::template bfly_l<E::IN>(a, b, A.F);
+        if (di) E::mul(b, w, A.F);
+        else E::template reduce<2 * E::IN, E::IN>(b, A.F);
+      }
+      E::template reduce<2 * E::IN, E::IN>(a, A.F);
+      lds_put_el<E>(u, i0, a);
+      lds_put_el<E>(u, i1, b);
+      __syncthreads();
+    }
+  }
+  // stores: the load map for v3 / v4 after the first round (consecutive k: coalesced), else the compute map
+  const bool rmap = V >= BEALTO_V3 && B.lgp != 0;
+  const size_t gi = rmap ? index_r : index, kk = rmap ? k_r : k;
+  const uint32_t li = rmap ? lid_r : lid;
+  const uint32_t* u = u_g + (size_t)(rmap ? gid_r : gid) * rl * E::W;
+  const size_t base = ((gi - kk) << deg) + kk;
+#pragma unroll
+  for (uint32_t j = 0; j < 2; ++j) {
+    const uint32_t i = li + j * lsz;
+    uint32_t v[E::W];
+    lds_get_el<E>(v, u, V == BEALTO_BELLPERSON ? i : brev_rt(i, deg));
+    E::template store<E::IN>(dst, base + i * p, v, A.F);
+  }
+}
+
+template <class E>
+hipError_t launch_bealto(int variant, const uint32_t* src, uint32_t* dst, const PassArgs<E>& A, const BealtoArgs& B,
+                         hipStream_t st) {
+  if constexpr (!HasStockham<E>::value) {
+    return hipErrorInvalidValue;
+  } else {
+    if (B.deg < 1 || B.deg > B.max_deg || B.deg > B.log_n || B.log_n - B.deg < B.log_g || src == dst)
+      return hipErrorInvalidValue;
+    const uint32_t threads = (1u << (B.deg - 1)) << B.log_g;
+    const size_t grid = ((size_t)1 << (B.log_n - B.deg)) >> B.log_g;
+    const size_t lds = ((size_t)((2u << (B.deg - 1)) + (variant == BEALTO_V4 ? 1u : 0u)) << B.log_g) * E::W * 4;
+    if (threads > 1024 || grid > 0x7fffffffull || lds > 64 * 1024) return hipErrorInvalidValue;
+    const dim3 g((uint32_t)grid), b(threads);
+    switch (variant) {
+      case BEALTO_BELLPERSON: hipLaunchKernelGGL((k_bealto<E, BEALTO_BELLPERSON>), g, b, lds, st, src, dst, A, B); break;
+      case BEALTO_V1: hipLaunchKernelGGL((k_bealto<E, BEALTO_V1>), g, b, lds, st, src, dst, A, B); break;
+      case BEALTO_V2: hipLaunchKernelGGL((k_bealto<E, BEALTO_V2>), g, b, lds, st, src, dst, A, B); break;
+      case BEALTO_V3: hipLaunchKernelGGL((k_bealto<E, BEALTO_V3>), g, b, lds, st, src, dst, A, B); break;
+      case BEALTO_V4: hipLaunchKernelGGL((k_bealto<E, BEALTO_V4>), g, b, lds, st, src, dst, A, B); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+}
+
 // k_build_tw's table as Shoup pairs: entry (c, k) = (w, floor(w B / p)) with w = w_n^((c*k) << log_m)
 // canonical, in the engine's twiddle format (E::TW words).  t = lo_s * hi = w B mod p; w = t / B
 // (Montgomery product by 1); floor(w B / p) = (-(w B mod p)) p^-1 mod B (shoup_ws29).
@@ -2207,6 +2332,8 @@ hipError_t launch_pointwise(const uint32_t* a, const uint32_t* b, uint32_t* c, s
   template hipError_t launch_naive_round<E>(const uint32_t*, uint32_t*, uint32_t, uint32_t, const uint32_t*,       \
                                             const typename E::Args&, hipStream_t);                                 \
   template hipError_t launch_noswap_round<E>(const uint32_t*, uint32_t*, uint32_t, uint32_t, const uint32_t*,      \
-                                             const typename E::Args&, hipStream_t);
+                                             const typename E::Args&, hipStream_t);                                 \
+  template hipError_t launch_bealto<E>(int, const uint32_t*, uint32_t*, const PassArgs<E>&, const BealtoArgs&,     \
+                                       hipStream_t);
 
 }  // namespace ntt

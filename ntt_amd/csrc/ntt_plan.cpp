@@ -35,6 +35,10 @@ namespace {
 
 thread_local int g_last_error = NTT_OK;
 
+// the bealto-family rival schedules (ntt.h): one k_bealto variant each
+constexpr unsigned kBealtoFlags = NTT_PLAN_BELLPERSON | NTT_PLAN_IMPROVED_V1 | NTT_PLAN_IMPROVED_V2 |
+                                  NTT_PLAN_IMPROVED_V3 | NTT_PLAN_IMPROVED_V4;
+
 // ------------------------------------------------------------------------------ single-launch order
 // The single launches (k_fused3 / k_fused3b / k_fused3bi / k_fused2b / k_fused2bi) wait across
 // workgroups, so each assumes its workgroups own the device: two of them enqueued on two streams could
@@ -546,6 +550,9 @@ struct PlanImpl final : PlanBase {
   uint32_t* d_stk_tab = nullptr;        // NTT_PLAN_STOCKHAM: per-pass input-twiddle tables
   uint32_t* d_naive_pw = nullptr;       // NTT_PLAN_NAIVE: w_n^i R_e, i < n/2 (the reference's `roots`)
   uint32_t* d_naive_buf = nullptr;      // NTT_PLAN_NAIVE: the bit-reversed copy the rounds work on
+                                        // (NO_SWAP, bealto family: the ping-pong partner of the caller's buffer)
+  size_t off_bealto_pq = 0;             // bealto family: w_{2^max_deg}^j, j < 2^(max_deg - 1), Shoup pairs
+  unsigned bealto_max_deg = 0, bealto_log_g = 0;
   size_t stk_off[8] = {};               // element offsets into d_stk_tab (pass >= 1)
   unsigned stk_ord[8] = {};             // Stockham pass i runs radix r[stk_ord[i]] (widest first)
   uint32_t* d_stk_buf[2] = {nullptr, nullptr};  // NTT_PLAN_STOCKHAM ping-pong buffers (E::MEMW words)
@@ -724,6 +731,14 @@ struct PlanImpl final : PlanBase {
         }
       }
     }
+    if ((flags & kBealtoFlags) && !twiddle_only) {
+      // the reference's pq table (GZKP-NTT.cu:489-499, 740-750): max_deg = min(8 - log_g, log_n), one
+      // group per workgroup for bellperson, 2^5 for the improved kernels (GZKP-NTT.cu:1674-1704)
+      if (log_n < 1) return NTT_ERR_ARG;
+      bealto_log_g = (flags & NTT_PLAN_BELLPERSON) ? 0u : 5u;
+      bealto_max_deg = std::min(8u - bealto_log_g, log_n);
+      off_bealto_pq = push_powers(H.pow_u64(w, n >> bealto_max_deg), 1ull << (bealto_max_deg - 1), nullptr);
+    }
     {  // pointwise product constants: mulv leaves a b / R_e (R_e the engine's Montgomery radix);
        // multiplying by R_e gives a b, by R_e R^-1 the Montgomery product a b R^-1 (R = 2^(64 limbs64))
       off_r2 = host.size();
@@ -778,6 +793,7 @@ struct PlanImpl final : PlanBase {
     // for k < 2^lgp_i is the GZKP DIT pass's w_N^(c d), N = 2^(lgp_i + r_i)
     if (rc == NTT_OK && (flags & (NTT_PLAN_STOCKHAM | NTT_PLAN_GZKP))) rc = build_stockham();
     if (rc == NTT_OK && (flags & (NTT_PLAN_NAIVE | NTT_PLAN_NO_SWAP))) rc = build_naive();
+    if (rc == NTT_OK && (flags & kBealtoFlags)) rc = build_bealto();
     (void)hipSetDevice(cur);
     return rc;
   }
@@ -906,6 +922,58 @@ struct PlanImpl final : PlanBase {
       e = hipMemcpyAsync(data, d_naive_buf, (size_t)n * MEMW * 4, hipMemcpyDeviceToDevice, st);
     mark(st);  // last_launch_ms: [all rounds (and the copy)]
     return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+  }
+
+  // NTT_PLAN_BELLPERSON / NTT_PLAN_IMPROVED_V1..V4 (rival schedules, the reference's bealto.com group
+  // FFT and its four refinements, GZKP-NTT.cu:391-464, 556-1296): rounds of 2^deg-point groups,
+  // deg = min(max_deg, log_n - lgp), one launch each (k_bealto), ping-pong between the caller's buffer
+  // and the plan buffer; an odd round count ends in the plan buffer and one device copy brings it back.
+  int build_bealto() {
+    if constexpr (!HasStockham<E>::value) {
+      return NTT_ERR_ARG;  // the rival schedules: P and 4 x 64-bit plans
+    } else {
+      if (log_n < 1 || log_n > 32 || bealto_max_deg < 1) return NTT_ERR_ARG;
+      if (hipMalloc(&d_naive_buf, (size_t)n * MEMW * 4) != hipSuccess) return NTT_ERR_HIP;
+      return NTT_OK;
+    }
+  }
+  int bealto_variant() const {
+    if (flags & NTT_PLAN_BELLPERSON) return BEALTO_BELLPERSON;
+    if (flags & NTT_PLAN_IMPROVED_V1) return BEALTO_V1;
+    if (flags & NTT_PLAN_IMPROVED_V2) return BEALTO_V2;
+    if (flags & NTT_PLAN_IMPROVED_V3) return BEALTO_V3;
+    return BEALTO_V4;
+  }
+  int run_bealto(uint32_t* data, hipStream_t st) {
+    if constexpr (!HasStockham<E>::value) {
+      return NTT_ERR_ARG;
+    } else {
+      const int variant = bealto_variant();
+      PassArgs<E> A = base_args(false);
+      A.tw_int = d_tab + off_bealto_pq;
+      A.tw_lo = d_tab + off_los_f;  // lo R_e: (lo R_e) hi, then the Montgomery product leaves x w
+      A.tw_hi = d_tab + off_hi_f;
+      BealtoArgs B{log_n, 0u, 0u, 0u, bealto_max_deg};
+      uint32_t* buf[2] = {data, d_naive_buf};
+      const unsigned nr = (log_n + bealto_max_deg - 1) / bealto_max_deg;
+      const bool per_round = nr + 2 < kEv;  // one profiling interval per round while they fit
+      const char* lab = variant == BEALTO_BELLPERSON ? "g" : "v";
+      begin(st);
+      hipError_t e = hipSuccess;
+      unsigned rounds = 0;
+      while (B.lgp < log_n && e == hipSuccess) {
+        B.deg = std::min(bealto_max_deg, log_n - B.lgp);
+        B.log_g = std::min(bealto_log_g, log_n - B.deg);
+        e = launch_bealto<E>(variant, buf[rounds & 1], buf[(rounds + 1) & 1], A, B, st);
+        if (per_round) mark(st, lab, B.deg);
+        B.lgp += B.deg;
+        ++rounds;
+      }
+      if (e == hipSuccess && (rounds & 1))
+        e = hipMemcpyAsync(data, d_naive_buf, (size_t)n * MEMW * 4, hipMemcpyDeviceToDevice, st);
+      if (!per_round || (rounds & 1)) mark(st, per_round ? "cp" : lab);
+      return e == hipSuccess ? NTT_OK : NTT_ERR_HIP;
+    }
   }
 
   int run_stockham(const uint32_t* in, uint32_t* out, hipStream_t st) {
@@ -1232,6 +1300,8 @@ struct PlanImpl final : PlanBase {
       return run_naive(static_cast<uint32_t*>(d), static_cast<uint32_t*>(d), st);
     if ((flags & NTT_PLAN_NO_SWAP) && !inverse && batch == 1 && d_naive_pw)
       return run_noswap(static_cast<uint32_t*>(d), st);
+    if ((flags & kBealtoFlags) && !inverse && batch == 1 && d_naive_buf)
+      return run_bealto(static_cast<uint32_t*>(d), st);
     return run_io(static_cast<uint32_t*>(d), nullptr, static_cast<uint32_t*>(d), batch, inverse, st);
   }
 
@@ -1918,7 +1988,7 @@ static int make_plan(std::unique_ptr<PlanBase>& out, const uint64_t* p64, const 
                      unsigned log_n, int device, unsigned flags) {
   if (log_n > 40) return NTT_ERR_ARG;
   if (limbs64 != 1 && limbs64 != 4 && limbs64 != 6) return NTT_ERR_ARG;  // before packing into p32[12] / g32[12]
-  const unsigned rivals = flags & (NTT_PLAN_STOCKHAM | NTT_PLAN_GZKP | NTT_PLAN_NAIVE | NTT_PLAN_NO_SWAP);
+  const unsigned rivals = flags & (NTT_PLAN_STOCKHAM | NTT_PLAN_GZKP | NTT_PLAN_NAIVE | NTT_PLAN_NO_SWAP | kBealtoFlags);
   if (rivals & (rivals - 1)) return NTT_ERR_ARG;  // one rival schedule per plan
   if ((flags & NTT_PLAN_IN_PLACE) && (rivals || (flags & NTT_PLAN_TWIDDLE_ONLY)))
     return NTT_ERR_ARG;

@@ -26,6 +26,11 @@ NTT_PLAN_IN_PLACE = 16
 NTT_PLAN_SINGLE_LAUNCH = 32
 NTT_PLAN_NAIVE = 64
 NTT_PLAN_NO_SWAP = 128
+NTT_PLAN_BELLPERSON = 256
+NTT_PLAN_IMPROVED_V1 = 512
+NTT_PLAN_IMPROVED_V2 = 1024
+NTT_PLAN_IMPROVED_V3 = 2048
+NTT_PLAN_IMPROVED_V4 = 4096
 
 # Every symbol declared in include/ntt.h with its ctypes prototype: (restype, argtypes).
 _vp = C.c_void_p

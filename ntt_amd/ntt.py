@@ -69,6 +69,10 @@ def from_device(t: torch.Tensor) -> List[int]:
     return out
 
 
+BEALTO_FLAGS = {"bellperson": _L.NTT_PLAN_BELLPERSON, "v1": _L.NTT_PLAN_IMPROVED_V1, "v2": _L.NTT_PLAN_IMPROVED_V2,
+                "v3": _L.NTT_PLAN_IMPROVED_V3, "v4": _L.NTT_PLAN_IMPROVED_V4}
+
+
 class NTTPlan:
     """A cached transform plan: twiddle tables and scratch live on the device.
 
@@ -81,8 +85,10 @@ class NTTPlan:
                  modulus: Optional[int] = None, generator: Optional[int] = None, twiddle_only: bool = False,
                  montgomery_io: bool = False, stockham: bool = False, gzkp: bool = False,
                  in_place: bool = False, single_launch: bool = False, naive: bool = False,
-                 no_swap: bool = False):
+                 no_swap: bool = False, bealto: str = ""):
         self._lib = _L.load()
+        if bealto and bealto not in BEALTO_FLAGS:
+            raise ValueError(f"bealto must be one of {sorted(BEALTO_FLAGS)}, not {bealto!r}")
         self.log_n = int(log_n)
         self.n = 1 << self.log_n
         self.limbs64 = int(limbs64)
@@ -102,6 +108,9 @@ class NTTPlan:
         flags |= _L.NTT_PLAN_NAIVE if naive else 0
         # no_swap: the reference's `naive_no_swap` rival (radix-2 Stockham autosort, one round per launch)
         flags |= _L.NTT_PLAN_NO_SWAP if no_swap else 0
+        # bealto: the reference's radix-2^deg group-FFT rivals -- "bellperson" (bellperson_baseline /
+        # FIELD_radix_fft_revised) or "v1".."v4" (improved_NTT_v1..v4), one k_bealto launch per round
+        flags |= BEALTO_FLAGS[bealto] if bealto else 0
         # in_place: no plan scratch, palindromic passes + tile-swap digit reversal (the reference's
         # self-sort-in-place property, GZKP-NTT.cu:1359-1449; ntt.h NTT_PLAN_IN_PLACE)
         flags |= _L.NTT_PLAN_IN_PLACE if in_place else 0

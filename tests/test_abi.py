@@ -145,7 +145,8 @@ def test_conflicting_schedule_flags_are_rejected_without_a_device():
     from ntt_amd import lib as L
     so = L.load()
     h = C.c_void_p()
-    rivals = (L.NTT_PLAN_STOCKHAM, L.NTT_PLAN_GZKP, L.NTT_PLAN_NAIVE, L.NTT_PLAN_NO_SWAP)
+    rivals = (L.NTT_PLAN_STOCKHAM, L.NTT_PLAN_GZKP, L.NTT_PLAN_NAIVE, L.NTT_PLAN_NO_SWAP, L.NTT_PLAN_BELLPERSON,
+              L.NTT_PLAN_IMPROVED_V1, L.NTT_PLAN_IMPROVED_V2, L.NTT_PLAN_IMPROVED_V3, L.NTT_PLAN_IMPROVED_V4)
     bad = [a | b for i, a in enumerate(rivals) for b in rivals[i + 1:]]
     bad += [r | L.NTT_PLAN_IN_PLACE for r in rivals] + [L.NTT_PLAN_IN_PLACE | L.NTT_PLAN_TWIDDLE_ONLY]
     for flags in bad:
