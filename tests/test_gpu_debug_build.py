@@ -34,7 +34,9 @@ def host(t, limbs):
 # clean runs: oracle parity at 2^14 and round trips, every engine; in place; polymul; batch
 for fid, lg, limbs, flags in ((1, 14, 4, {}), (2, 14, 6, {}), (0, 14, 1, {}), (1, 20, 4, {}), (2, 18, 4, {}),
                               (0, 22, 1, {}), (1, 20, 4, {"in_place": True}), (0, 20, 1, {"in_place": True}),
-                              (1, 20, 4, {"single_launch": True})):
+                              (1, 20, 4, {"single_launch": True}), (1, 14, 4, {"bealto": "bellperson"}),
+                              (1, 14, 4, {"bealto": "v3"}), (0, 14, 1, {"bealto": "v4"}), (2, 14, 4, {"bealto": "v1"}),
+                              (1, 14, 4, {"no_swap": True}), (0, 14, 1, {"naive": True})):
     pl = NTTPlan(fid, lg, limbs, **flags)
     t = pl.fill(pl.empty(), "random", seed=3)
     x = t.clone()

@@ -114,3 +114,38 @@ def test_count_noncanonical(fid, L):
     t[5:9] = bad
     t[20] = -1  # all limbs 0xffff...: not a residue in any layout
     assert pl.count_noncanonical(t) == 4
+
+
+RIVAL_SCHEDULES = ["stockham", "gzkp", "naive", "no_swap", "bellperson", "v1", "v2", "v3", "v4"]
+
+
+@pytest.mark.parametrize("sched", RIVAL_SCHEDULES)
+@pytest.mark.parametrize("fid,L", [(1, 4), (2, 4), (0, 1)])
+def test_rival_schedules_on_edge_vectors(fid, L, sched):
+    """The rival schedules (test_gpu_rivals.py) on the same adversarial inputs: near-p patterns against
+    the oracle, and the constant p - 1 (X_0 = n (p - 1), the rest 0); through the checked build no
+    lazy-bound or output check may fire (k_bealto's rounds keep < 4p between LDS stages)."""
+    from ntt_amd.ntt import NTTPlan
+    p, g = R.FIELDS[fid]
+    for log_n in (12, 16):
+        n = 1 << log_n
+        pl = NTTPlan(field_id=fid, log_n=log_n, limbs64=L, device=0, stockham=sched == "stockham",
+                     gzkp=sched == "gzkp", naive=sched == "naive", no_swap=sched == "no_swap",
+                     bealto=sched if sched in ("bellperson", "v1", "v2", "v3", "v4") else "")
+        rng = np.random.default_rng(log_n + 3)
+        pattern = rng.integers(0, 4, n)
+        vals = [(p - 1, p - 2, 0, p - 1 - int(rng.integers(0, 1 << 20)))[int(s)] for s in pattern]
+        x = _limbs(vals, L)
+        got = _run(pl, x) if L > 1 else _run1(pl, x)
+        assert np.array_equal(got, OC.ntt_mp(x, p, g, False)), (fid, L, log_n, sched)
+        c = _const_limbs(p - 1, n, L)
+        got = _run(pl, c) if L > 1 else _run1(pl, c)
+        assert _values(got[:1]) == [n * (p - 1) % p] and not got[1:].any(), (fid, L, log_n, sched)
+
+
+def _run1(pl, host):
+    """_run for the 1-limb (`long long`) layout: a flat tensor"""
+    t = torch.from_numpy(np.ascontiguousarray(host[:, 0]).view(np.int64)).to("cuda:0")
+    pl.forward(t)
+    assert pl.device_status() == 0, hex(pl.device_status())
+    return t.cpu().numpy().view(np.uint64).reshape(host.shape)
