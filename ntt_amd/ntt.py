@@ -86,9 +86,9 @@ class NTTPlan:
                  montgomery_io: bool = False, stockham: bool = False, gzkp: bool = False,
                  in_place: bool = False, single_launch: bool = False, naive: bool = False,
                  no_swap: bool = False, bealto: str = ""):
-        self._lib = _L.load()
         if bealto and bealto not in BEALTO_FLAGS:
             raise ValueError(f"bealto must be one of {sorted(BEALTO_FLAGS)}, not {bealto!r}")
+        self._lib = _L.load()
         self.log_n = int(log_n)
         self.n = 1 << self.log_n
         self.limbs64 = int(limbs64)

@@ -152,3 +152,16 @@ def test_conflicting_schedule_flags_are_rejected_without_a_device():
     for flags in bad:
         assert so.ntt_plan_create_ex(C.byref(h), 1, 12, 4, 0, flags) == L.NTT_ERR_ARG, flags
         assert not h.value
+
+
+def test_bealto_kwarg_is_checked_before_the_library():
+    """NTTPlan(bealto=...) names one of the five bealto-family schedules; anything else is refused
+    before a plan (or a device) is touched."""
+    import pytest as _pt
+    from ntt_amd import lib as L
+    from ntt_amd.ntt import BEALTO_FLAGS, NTTPlan
+    assert BEALTO_FLAGS == {"bellperson": L.NTT_PLAN_BELLPERSON, "v1": L.NTT_PLAN_IMPROVED_V1,
+                            "v2": L.NTT_PLAN_IMPROVED_V2, "v3": L.NTT_PLAN_IMPROVED_V3, "v4": L.NTT_PLAN_IMPROVED_V4}
+    for bad in ("v0", "v5", "Bellperson", "stockham"):
+        with _pt.raises(ValueError):
+            NTTPlan(1, 12, 4, bealto=bad)
